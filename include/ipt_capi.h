@@ -1,0 +1,178 @@
+/* ipt_capi.h — C-ABI of the MI355X path-tracing inner loop (libipt_hip.so).
+ *
+ * This is the drop-in boundary for dimalit/ipt's hot path. The reference has
+ * no FFI; its boundary is a set of C++ virtual interfaces called per ray
+ * (reference src/tracer_interfaces.h:26-54) driven by
+ *   render_sample(const Scene&, RenderPlane&, StatsNode*)   src/main.cpp:186-223
+ *   ray_power_recursive(...)                                 src/main.cpp:98-184
+ * Per-ray virtual calls cannot cross to a GPU, so this ABI works at frame
+ * granularity: the caller flattens a Scene (camera + geometry + lights) into
+ * the POD structs below once, then asks for whole sample passes.
+ *
+ * Conventions: plain pointers and sizes, no exceptions, every call returns
+ * IPT_OK (0) or a negative IPT_E_* code, the message of the last failure is
+ * available from ipt_last_error(). Calls are synchronous unless they take a
+ * stream argument. One context per HIP device; contexts are independent, a
+ * single context is not reentrant. There is NO CPU fallback: without a usable
+ * gfx950 device every rendering call fails with IPT_E_DEVICE.
+ */
+#ifndef IPT_CAPI_H
+#define IPT_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPT_ABI_VERSION 1
+
+enum {
+    IPT_OK = 0,
+    IPT_E_INVALID = -1,     /* bad argument / size / pointer */
+    IPT_E_DEVICE = -2,      /* HIP runtime or device failure, no gfx950 device */
+    IPT_E_UNSUPPORTED = -3, /* scene or parameter outside what the kernels implement */
+    IPT_E_NOSCENE = -4,     /* ipt_render before ipt_upload_scene */
+    IPT_E_OOM = -5
+};
+
+/* Geometry kinds (reference src/geometry/). */
+enum {
+    /* GeometrySphereInBox (GeometrySphereInBox.cpp:10-81): planes
+       {+x,+y,+z,-x,-z} of the cube [-1,1]^3 (no -y wall) then a sphere of
+       radius 0.5 at the origin. The sample_scenes[0] geometry. */
+    IPT_GEOM_SPHERE_IN_BOX = 0,
+    /* The same five box planes followed by N extra spheres scanned in order
+       with FractalSpheres' acceptance rule (FractalSpheres.cpp:75-84); the
+       10k-primitive stress configuration of BASELINE.json configs[2]. */
+    IPT_GEOM_SPHERES_IN_BOX = 1
+};
+
+/* Light kinds (reference src/lighting/lighting.h). */
+enum { IPT_LIGHT_AREA_DIAMOND = 0, IPT_LIGHT_AREA_TRIANGLE = 1 };
+
+/* AreaLight constructor arguments (lighting.cpp:79-90); derived fields
+   (area, normal, inverse_matrix, surface power) are computed by
+   ipt_upload_scene with the constructor's own float operation order. */
+typedef struct ipt_area_light {
+    float position[3]; /* Light::position, the corner */
+    float x_axis[3];
+    float y_axis[3];
+    float power;
+    int32_t type; /* IPT_LIGHT_AREA_* */
+} ipt_area_light;
+
+/* SimpleCamera public fields after construction (SimpleCamera.h:11-13). */
+typedef struct ipt_camera {
+    float position[3];
+    float direction[3];
+    float right[3];
+    float up[3];
+} ipt_camera;
+
+typedef struct ipt_sphere {
+    float center[3];
+    float radius;
+} ipt_sphere;
+
+typedef struct ipt_scene {
+    int32_t geometry_kind;     /* IPT_GEOM_* */
+    int32_t n_lights;          /* CollectionLighting::lights, insertion order */
+    const ipt_area_light* lights;
+    int32_t n_spheres;         /* extra spheres for IPT_GEOM_SPHERES_IN_BOX */
+    const ipt_sphere* spheres;
+    ipt_camera camera;
+} ipt_scene;
+
+typedef struct ipt_params {
+    int32_t width, height;  /* GridRenderPlane size; render_sample hardcodes 640x640 */
+    int32_t spp;            /* number of render_sample passes in this call */
+    int32_t spp_offset;     /* absolute index of the first pass (RNG counter) */
+    int32_t n_rays;         /* branching factor of the root node (main.cpp:94), 1..64 */
+    int32_t depth_max;      /* main.cpp:95 */
+    uint64_t seed;          /* Philox key */
+    /* Destination-row sharding across devices: rows are cut into tiles of
+       tile_rows rows, tile t belongs to shard t % n_shards. n_shards <= 1 or
+       tile_rows <= 0 means this call owns the whole frame. */
+    int32_t tile_rows;
+    int32_t n_shards;
+    int32_t shard_id;
+    uint32_t flags;         /* IPT_FLAG_* */
+} ipt_params;
+
+enum {
+    IPT_FLAG_COUNTERS = 1u /* accumulate ipt_counters during the call */
+};
+
+/* Caller-owned GridRenderPlane state (GridRenderPlane.h:9-12), width*height
+   row-major each. ipt_render ACCUMULATES into it with GridRenderPlane::addRay's
+   running-mean update (GridRenderPlane.cpp:61-75), sample passes in order and
+   each pass in render_sample's raster order, so repeated calls with increasing
+   spp_offset continue the same image bit-for-bit. Zero-initialise before the
+   first call. `sums` (sequential per-pixel sum in the same order) and
+   `pixel_max` (per-pixel running maximum; GridRenderPlane::max_value is its
+   maximum over the frame) may be NULL. */
+typedef struct ipt_image {
+    float* pixels;
+    uint32_t* counters;
+    float* sums;
+    float* pixel_max;
+} ipt_image;
+
+/* Event counters (SURVEY.md Appendix C vocabulary), summed over the call. */
+typedef struct ipt_counters {
+    uint64_t paths;           /* root ray_power calls */
+    uint64_t traced_rays;     /* Geometry::traceRay calls */
+    uint64_t surface_hits;    /* rays whose nearest visible hit is geometry */
+    uint64_t light_hits;      /* rays returning a light's power */
+    uint64_t expanded_nodes;  /* nodes that ran the branch loop (n_rays > 0) */
+    uint64_t iterations;      /* UnionDdf::sample calls */
+    uint64_t light_samples;   /* iterations that sampled a light component */
+    uint64_t skipped;         /* iterations that returned vec3() */
+    uint64_t sphere_frames;   /* RotateDdf builds at non-wall normals */
+    uint64_t light_traces;    /* AreaLight::traceRay calls */
+    uint64_t drifted;         /* samples GridRenderPlane maps off their nominal pixel */
+} ipt_counters;
+
+typedef struct ipt_ctx ipt_ctx;
+
+int ipt_abi_version(void);
+const char* ipt_last_error(ipt_ctx* ctx); /* ctx may be NULL (creation errors) */
+
+int ipt_create(int hip_device, ipt_ctx** out);
+void ipt_destroy(ipt_ctx* ctx);
+
+/* Copies the scene (caller keeps ownership of its arrays). */
+int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* scene);
+
+/* Host buffers: copies the image in, renders p->spp passes, copies it out. */
+int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* host_img);
+
+/* Device buffers (hipMalloc'd or torch CUDA tensors) on `hip_stream`
+   (NULL = the context's own stream). Asynchronous w.r.t. the host. */
+int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, void* hip_stream);
+
+/* Per-sample radiance, for bit-exact verification: values[s][iy][ix] is the
+   clamped root ray_power of pass p->spp_offset+s at source pixel (ix,iy)
+   (main.cpp:211-214) and codes[s][iy][ix] the GridRenderPlane drift code
+   (bits 0-1: dx+1, bits 2-3: dy+1 relative to the nominal destination
+   (ix, max(H-2-iy,0)); 0x05 = nominal). Host buffers of spp*width*height. */
+int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t* codes);
+
+int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out);
+int ipt_reset_counters(ipt_ctx* ctx);
+
+/* Timing of the most recent render call's kernels (ms, HIP events on the
+   launch stream): [0] = path kernel, [1] = accumulate kernel. */
+int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
+
+/* ---- portable-math probes (same code as the kernels), for tests ---------
+   fn: 0 acosf, 1 sinf, 2 cosf, 3 (float)acos((double)x), 4 sincosf->sin,
+       5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u)      */
+int ipt_math_host(int fn, const float* in, float* out, int64_t n);
+int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPT_CAPI_H */

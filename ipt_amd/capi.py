@@ -1,0 +1,249 @@
+"""ctypes binding of include/ipt_capi.h (libipt_hip.so).
+
+This is the Python-side view of the drop-in boundary: the same entry points a
+cgo / JNI / ctypes caller of the reference would bind.
+Only plain pointers cross it. The library has no CPU fallback: every rendering
+call needs a gfx950 device and fails loudly (IptError) otherwise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "lib" / "libipt_hip.so"
+
+IPT_OK = 0
+IPT_E_INVALID = -1
+IPT_E_DEVICE = -2
+IPT_E_UNSUPPORTED = -3
+IPT_E_NOSCENE = -4
+IPT_E_OOM = -5
+
+IPT_GEOM_SPHERE_IN_BOX = 0
+IPT_GEOM_SPHERES_IN_BOX = 1
+IPT_LIGHT_AREA_DIAMOND = 0
+IPT_LIGHT_AREA_TRIANGLE = 1
+IPT_FLAG_COUNTERS = 1
+
+F3 = C.c_float * 3
+
+
+class AreaLight(C.Structure):
+    _fields_ = [("position", F3), ("x_axis", F3), ("y_axis", F3), ("power", C.c_float),
+                ("type", C.c_int32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("position", F3), ("direction", F3), ("right", F3), ("up", F3)]
+
+
+class Sphere(C.Structure):
+    _fields_ = [("center", F3), ("radius", C.c_float)]
+
+
+class Scene(C.Structure):
+    _fields_ = [("geometry_kind", C.c_int32), ("n_lights", C.c_int32),
+                ("lights", C.POINTER(AreaLight)), ("n_spheres", C.c_int32),
+                ("spheres", C.POINTER(Sphere)), ("camera", Camera)]
+
+
+class Params(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
+                ("spp_offset", C.c_int32), ("n_rays", C.c_int32), ("depth_max", C.c_int32),
+                ("seed", C.c_uint64), ("tile_rows", C.c_int32), ("n_shards", C.c_int32),
+                ("shard_id", C.c_int32), ("flags", C.c_uint32)]
+
+
+class Image(C.Structure):
+    _fields_ = [("pixels", C.c_void_p), ("counters", C.c_void_p), ("sums", C.c_void_p),
+                ("pixel_max", C.c_void_p)]
+
+
+COUNTER_NAMES = ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
+                 "iterations", "light_samples", "skipped", "sphere_frames", "light_traces",
+                 "drifted")
+
+
+class Counters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in COUNTER_NAMES}
+
+
+EXPORTED_SYMBOLS = (
+    "ipt_abi_version", "ipt_last_error", "ipt_create", "ipt_destroy", "ipt_upload_scene",
+    "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
+    "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
+)
+
+_lib = None
+
+
+class IptError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"ipt error {code}: {msg}")
+        self.code = code
+
+
+def load(path: str | os.PathLike | None = None):
+    """Load libipt_hip.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise IptError(IPT_E_DEVICE, f"{p} is not built; run __graft_entry__.build()")
+    lib = C.CDLL(str(p))
+    lib.ipt_abi_version.restype = C.c_int
+    lib.ipt_last_error.restype = C.c_char_p
+    lib.ipt_last_error.argtypes = [C.c_void_p]
+    lib.ipt_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    lib.ipt_destroy.argtypes = [C.c_void_p]
+    lib.ipt_destroy.restype = None
+    lib.ipt_upload_scene.argtypes = [C.c_void_p, C.POINTER(Scene)]
+    lib.ipt_render.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(Image)]
+    lib.ipt_render_device.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(Image), C.c_void_p]
+    lib.ipt_render_values.argtypes = [C.c_void_p, C.POINTER(Params), C.c_void_p, C.c_void_p]
+    lib.ipt_get_counters.argtypes = [C.c_void_p, C.POINTER(Counters)]
+    lib.ipt_reset_counters.argtypes = [C.c_void_p]
+    lib.ipt_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    lib.ipt_math_host.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
+    lib.ipt_math_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(lib, ctx, rc):
+    if rc != IPT_OK:
+        raise IptError(rc, lib.ipt_last_error(ctx).decode(errors="replace"))
+
+
+def make_scene(desc: dict) -> tuple[Scene, list]:
+    """Build an ipt_scene from the dict produced by ipt_amd.scenes; returns the
+    struct and the Python objects that keep its arrays alive."""
+    lights = desc.get("lights", [])
+    la = (AreaLight * max(len(lights), 1))()
+    for i, L in enumerate(lights):
+        la[i].position[:] = L["position"]
+        la[i].x_axis[:] = L["x_axis"]
+        la[i].y_axis[:] = L["y_axis"]
+        la[i].power = L["power"]
+        la[i].type = L.get("type", IPT_LIGHT_AREA_DIAMOND)
+    spheres = desc.get("spheres", [])
+    sa = (Sphere * max(len(spheres), 1))()
+    for i, (c, r) in enumerate(spheres):
+        sa[i].center[:] = c
+        sa[i].radius = r
+    cam = desc["camera"]
+    s = Scene()
+    s.geometry_kind = desc["geometry_kind"]
+    s.n_lights = len(lights)
+    s.lights = C.cast(la, C.POINTER(AreaLight))
+    s.n_spheres = len(spheres)
+    s.spheres = C.cast(sa, C.POINTER(Sphere))
+    s.camera.position[:] = cam["position"]
+    s.camera.direction[:] = cam["direction"]
+    s.camera.right[:] = cam["right"]
+    s.camera.up[:] = cam["up"]
+    return s, [la, sa]
+
+
+def make_params(width, height, spp, spp_offset=0, n_rays=16, depth_max=8, seed=20241223,
+                tile_rows=0, n_shards=1, shard_id=0, flags=0) -> Params:
+    p = Params()
+    p.width, p.height, p.spp, p.spp_offset = width, height, spp, spp_offset
+    p.n_rays, p.depth_max, p.seed = n_rays, depth_max, seed
+    p.tile_rows, p.n_shards, p.shard_id, p.flags = tile_rows, n_shards, shard_id, flags
+    return p
+
+
+class Context:
+    """One ipt_ctx on one HIP device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.ipt_create(device, C.byref(h))
+        if rc != IPT_OK:
+            raise IptError(rc, self.lib.ipt_last_error(None).decode(errors="replace"))
+        self.h = h
+        self._keep = None
+
+    def close(self):
+        if self.h:
+            self.lib.ipt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_scene(self, desc: dict):
+        s, keep = make_scene(desc)
+        _check(self.lib, self.h, self.lib.ipt_upload_scene(self.h, C.byref(s)))
+        self._keep = keep
+
+    def render_values(self, p: Params):
+        n = p.spp * p.width * p.height
+        vals = np.zeros(n, np.float32)
+        codes = np.zeros(n, np.uint8)
+        _check(self.lib, self.h, self.lib.ipt_render_values(
+            self.h, C.byref(p), vals.ctypes.data, codes.ctypes.data))
+        shape = (p.spp, p.height, p.width)
+        return vals.reshape(shape), codes.reshape(shape)
+
+    def render(self, p: Params, img: dict):
+        """Host-buffer render into img = {pixels, counters, sums?, pixel_max?} (numpy)."""
+        im = Image()
+        im.pixels = img["pixels"].ctypes.data
+        im.counters = img["counters"].ctypes.data
+        im.sums = img["sums"].ctypes.data if img.get("sums") is not None else None
+        im.pixel_max = img["pixel_max"].ctypes.data if img.get("pixel_max") is not None else None
+        _check(self.lib, self.h, self.lib.ipt_render(self.h, C.byref(p), C.byref(im)))
+
+    def render_device(self, p: Params, pixels_ptr, counters_ptr, sums_ptr=None, max_ptr=None,
+                      stream=None):
+        im = Image()
+        im.pixels, im.counters, im.sums, im.pixel_max = pixels_ptr, counters_ptr, sums_ptr, max_ptr
+        _check(self.lib, self.h, self.lib.ipt_render_device(self.h, C.byref(p), C.byref(im), stream))
+
+    def counters(self) -> dict:
+        c = Counters()
+        _check(self.lib, self.h, self.lib.ipt_get_counters(self.h, C.byref(c)))
+        return c.as_dict()
+
+    def reset_counters(self):
+        _check(self.lib, self.h, self.lib.ipt_reset_counters(self.h))
+
+    def last_kernel_ms(self):
+        a, b = C.c_float(), C.c_float()
+        _check(self.lib, self.h, self.lib.ipt_last_kernel_ms(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def math_device(self, fn: int, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.empty_like(x)
+        _check(self.lib, self.h, self.lib.ipt_math_device(self.h, fn, x.ctypes.data, out.ctypes.data, x.size))
+        return out
+
+
+def math_host(fn: int, x: np.ndarray) -> np.ndarray:
+    lib = load()
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    rc = lib.ipt_math_host(fn, x.ctypes.data, out.ctypes.data, x.size)
+    if rc != IPT_OK:
+        raise IptError(rc, "ipt_math_host")
+    return out
+
+
+MATH_FNS = {"acosf": 0, "sinf": 1, "cosf": 2, "acos_f64_f32": 3, "sincosf_sin": 4,
+            "sincosf_cos": 5, "sqrtf": 6, "div_pi": 7, "two_pi_times": 8}

@@ -1,0 +1,993 @@
+// ipt_kernels.hip — gfx950 kernels and the C-ABI (include/ipt_capi.h) of the
+// ipt path-tracing inner loop.
+//
+// Kernels
+//   path_kernel        persistent megakernel: one lane = one path (camera
+//                      sample) at a time; the reference's recursive branching
+//                      estimator (main.cpp:98-184) runs as an explicit DFS
+//                      with the suspended ancestors in LDS and the current
+//                      node in registers; lanes refill from a wave-local pool
+//                      of work units fed by one global atomic per 256 units.
+//                      Writes the per-sample radiance + GridRenderPlane drift
+//                      code of every (pass, source pixel).
+//   accumulate_kernel  one thread per destination pixel: replays
+//                      GridRenderPlane::addRay (GridRenderPlane.cpp:61-75) for
+//                      all passes in render_sample order — coalesced reads of
+//                      the radiance buffer, HBM-bound.
+// Build: see __graft_entry__.py (hipcc --offload-arch=gfx950 -O3
+//        -ffp-contract=off, no fast-math).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ipt_capi.h"
+#include "ipt_path.h"
+
+using namespace ipt;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kStackFields = 18;  // pos3, frame12, res, mult, i
+constexpr int kPoolChunk = 256;   // work units per global atomic
+constexpr int kNumCounters = 11;
+
+struct KParams {
+    int W, H, spp, spp_offset, n_rays, depth_max;
+    uint32_t key0, key1;
+    int n_cand;              // candidate source rows
+    const int* cand_rows;    // [n_cand] source row index
+    int tile_rows, n_shards, shard_id;
+    unsigned long long total_units;
+    unsigned long long* unit_counter;
+    float* values;           // [spp][n_cand][W]
+    uint8_t* codes;          // [spp][n_cand][W]
+    uint8_t* flags;          // [H][W]
+    unsigned long long* counters;
+    int geometry_kind;
+    int n_lights;
+    const LightDev* lights;  // [n_lights]
+    const float* weights;    // [n_lights+1]
+    const float* cdf;        // [n_lights+1] sequential prefix sums of weights
+    const Frame* wall_frames;  // [5]
+    vec3 cam_pos, cam_dir, cam_right, cam_up;
+    int n_spheres;
+    const float4* spheres;   // (c.xyz, r)
+};
+
+__device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
+    if (kp.n_shards <= 1 || kp.tile_rows <= 0) return true;
+    return ((yi / kp.tile_rows) % kp.n_shards) == kp.shard_id;
+}
+
+// 8-word RNG window (blocks blk and blk+1 of the path's Philox stream) in
+// named registers; draws are picked with selects (a runtime-indexed array
+// would be placed in scratch).
+struct Win8 {
+    uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+};
+__device__ __forceinline__ uint32_t win_at(const Win8& w, uint32_t j) {
+    // j in [0,6)
+    uint32_t lo = j == 0 ? w.a0 : (j == 1 ? w.a1 : (j == 2 ? w.a2 : w.a3));
+    uint32_t hi = j == 4 ? w.b0 : w.b1;
+    return j < 4 ? lo : hi;
+}
+
+__device__ __forceinline__ void philox_fill(uint32_t& d0, uint32_t& d1, uint32_t& d2, uint32_t& d3,
+                                            uint32_t blk, uint32_t pass, uint32_t pix, uint32_t k0,
+                                            uint32_t k1) {
+    u32x4 o = philox4x32_10(blk, pass, pix, 0u, k0, k1);
+    d0 = o.v[0];
+    d1 = o.v[1];
+    d2 = o.v[2];
+    d3 = o.v[3];
+}
+
+// Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
+// r=0.5 sphere, 6 an extra sphere (center in *sc), -1 miss.
+__device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim,
+                                                vec3* sc) {
+    if (kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
+    // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
+    int p;
+    float best = trace_box_planes_only(o, d, &p);
+    for (int i = 0; i < kp.n_spheres; ++i) {
+        float4 s = kp.spheres[i];
+        vec3 c = v3(s.x, s.y, s.z);
+        float t = sphere_t(s.w, o - c, d);
+        if (isfinite_(t) && gt_1em6(fabs_(t)) && t < best) {
+            best = t;
+            p = 6;
+            *sc = c;
+        }
+    }
+    *prim = p;
+    return best;
+}
+
+template <int MAXSUSP, bool COUNT>
+__global__ __launch_bounds__(kBlock, 2) void path_kernel(KParams kp) {
+    extern __shared__ float lds[];
+    float* stk = lds;                                         // [MAXSUSP][F][kBlock]
+    float* wallf = lds + MAXSUSP * kStackFields * kBlock;     // [5][12]
+    const int tid = threadIdx.x;
+    if (tid < 60) wallf[tid] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int nl = kp.n_lights;
+    const float w_sdf = kp.weights[nl];
+    const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
+
+    // wave-local unit pool (uniform)
+    unsigned long long pool_next = 0, pool_end = 0;
+
+    // lane state
+    bool active = true, has_path = false;
+    unsigned long long unit = 0;
+    uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
+    Win8 w;
+    vec3 tpos = v3(0, 0, 0);
+    Frame tfr;
+    float tres = 0.0f;
+    int ti = 0, tdepth = 0;
+    int dest_x = 0, dest_y = 0;
+    uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
+             c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0;
+
+    for (;;) {
+        // -------------------------------------------------- unit refill
+        const bool need = active && !has_path;
+        const uint64_t needmask = __ballot(need);
+        if (needmask) {
+            const int cnt = __popcll(needmask);
+            const int rank = __popcll(needmask & lanemask_lt);
+            unsigned long long avail = pool_end - pool_next;
+            unsigned long long my = 0;
+            if ((unsigned long long)cnt > avail) {
+                unsigned long long base = 0;
+                if (lane == __ffsll((long long)needmask) - 1)
+                    base = atomicAdd(kp.unit_counter, (unsigned long long)kPoolChunk);
+                base = __shfl(base, __ffsll((long long)needmask) - 1);
+                if ((unsigned long long)rank < avail)
+                    my = pool_next + rank;
+                else
+                    my = base + (rank - avail);
+                pool_next = base + (cnt - avail);
+                pool_end = base + kPoolChunk;
+            } else {
+                my = pool_next + rank;
+                pool_next += cnt;
+            }
+            if (need) {
+                if (my >= kp.total_units) {
+                    active = false;
+                } else {
+                    unit = my;
+                    has_path = true;
+                    tdepth = -1;  // marks "camera ray pending"
+                }
+            }
+        }
+        if (__ballot(active) == 0) break;
+
+        // -------------------------------------------------- advance phase
+        bool have_ray = false, is_iter = false;
+        vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
+        int rdepth = 0;
+        float sdf_val = 0.0f;
+
+        if (active && has_path && tdepth == -1) {
+            // new path: render_sample pixel body (main.cpp:192-211)
+            const unsigned long long s = unit / per_pass;
+            const unsigned long long rem = unit - s * per_pass;
+            const int cand = (int)(rem / (unsigned long long)kp.W);
+            const int ix = (int)(rem - (unsigned long long)cand * kp.W);
+            const int iy = kp.cand_rows[cand];
+            rpass = (uint32_t)(kp.spp_offset + (int)s);
+            rpix = (uint32_t)(iy * kp.W + ix);
+            philox_fill(w.a0, w.a1, w.a2, w.a3, 0u, rpass, rpix, kp.key0, kp.key1);
+            philox_fill(w.b0, w.b1, w.b2, w.b3, 1u, rpass, rpix, kp.key0, kp.key1);
+            blk = 0;
+            k = 2;
+            const float x = jitter_coord(ix, u01(w.a0), kp.W);
+            const float y = jitter_coord(iy, u01(w.a1), kp.H);
+            int xi, yi;
+            grid_index(x, y, kp.W, kp.H, &xi, &yi);
+            const int yn = nominal_row(iy, kp.H);
+            const int dx = xi - ix, dy = yi - yn;
+            uint8_t code = 0xff;
+            if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < kp.W && yi < kp.H)
+                code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
+            kp.codes[unit] = code;
+            dest_x = xi;
+            dest_y = yi;
+            if (code != 0x05 && code != 0xff) {
+                kp.flags[(size_t)yn * kp.W + ix] = 1;
+                kp.flags[(size_t)yi * kp.W + xi] = 1;
+                if (COUNT) ++c_drift;
+            }
+            if (code == 0xff || !owned_row(kp, yi)) {
+                // not ours (halo row of another shard) or out of range
+                kp.values[unit] = 0.0f;
+                if (code != 0xff) kp.codes[unit] = 0xfe;
+                has_path = false;
+            } else {
+                ro = kp.cam_pos;
+                rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
+                rdepth = 0;
+                have_ray = true;
+                if (COUNT) ++c_paths;
+            }
+        } else if (active && has_path) {
+            // finalize finished nodes (main.cpp:181) and pop (main.cpp:177)
+            for (;;) {
+                const int n = kp.n_rays >> tdepth;
+                if (ti < n) break;
+                const float v = isfinite_(tres) ? tres / (float)n : 0.0f;
+                if (tdepth == 0) {
+                    const float val = v >= 0.0f ? v : 0.0f;  // main.cpp:214
+                    kp.values[unit] = val;
+                    has_path = false;
+                    break;
+                }
+                const int lvl = tdepth - 1;
+                float* b = stk + (size_t)lvl * kStackFields * kBlock + tid;
+                tpos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
+                tfr.m0 = v3(b[3 * kBlock], b[4 * kBlock], b[5 * kBlock]);
+                tfr.m1 = v3(b[6 * kBlock], b[7 * kBlock], b[8 * kBlock]);
+                tfr.m2 = v3(b[9 * kBlock], b[10 * kBlock], b[11 * kBlock]);
+                tfr.iz = v3(b[12 * kBlock], b[13 * kBlock], b[14 * kBlock]);
+                const float pres = b[15 * kBlock];
+                const float pmult = b[16 * kBlock];
+                ti = __float_as_int(b[17 * kBlock]);
+                tres = pres + (pmult * 1.0f) * v;  // res += multiplier*albedo*ray_power
+                tdepth = lvl;
+            }
+            if (has_path) {
+                // one iteration of the branch loop (main.cpp:149-178)
+                if ((k >> 2) != blk) {
+                    w.a0 = w.b0; w.a1 = w.b1; w.a2 = w.b2; w.a3 = w.b3;
+                    ++blk;
+                    philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
+                }
+                const uint32_t j = k - 4 * blk;
+                const float r = u01(win_at(w, j));
+                // UnionDdf::sample pick (ddf.cpp:142-153): first c with r < cdf[c]
+                int c = 0;
+                while (c <= nl && !(r < kp.cdf[c])) ++c;
+                vec3 dir = v3(0, 0, 0);
+                if (c <= nl) {
+                    const float u1 = u01(win_at(w, j + 1));
+                    const float u2 = u01(win_at(w, j + 2));
+                    k += 3;
+                    if (c < nl) {
+                        dir = light_sample_dir(kp.lights[c], tpos, u1, u2);
+                        if (COUNT) ++c_lsamp;
+                    } else {
+                        dir = frame_apply(tfr, cosine_sample_local(u1, u2));
+                    }
+                } else {
+                    k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
+                }
+                ++ti;
+                if (COUNT) ++c_iter;
+                if (is_zero(dir)) {
+                    if (COUNT) ++c_skip;
+                } else {
+                    ro = tpos;
+                    rd = dir;
+                    rdepth = tdepth + 1;
+                    have_ray = true;
+                    is_iter = true;
+                }
+            }
+        }
+
+        // -------------------------------------------------- trace phase
+        if (have_ray) {
+            // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
+            // and the child's CollectionLighting::traceRayToLight
+            float lmix = 0.0f;
+            bool has_li = false;
+            vec3 li_pos = v3(0, 0, 0);
+            float li_pow = 0.0f;
+            for (int l = 0; l < nl; ++l) {
+                const LightDev& L = kp.lights[l];
+                vec3 hp;
+                const bool h = light_trace(L, ro, rd, &hp);
+                if (COUNT) c_ltr += (is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u);
+                if (is_iter) lmix += kp.weights[l] * light_pdf(L, ro, h, hp);
+                if (h && (!has_li || length(li_pos - ro) > length(hp - ro))) {
+                    has_li = true;
+                    li_pos = hp;
+                    li_pow = L.spow;
+                }
+            }
+            float mult = 0.0f;
+            if (is_iter) {
+                sdf_val = frame_cosine_value(tfr, rd);
+                const float mix = lmix + w_sdf * sdf_val;
+                mult = sdf_val / mix;
+            }
+            // child ray_power (main.cpp:100-143)
+            float cv = 0.0f;
+            bool push = false;
+            vec3 si_pos = v3(0, 0, 0), sph_c = v3(0, 0, 0);
+            int prim = -1;
+            if (rdepth < kp.depth_max) {
+                const float t = trace_geometry(kp, ro, rd, &prim, &sph_c);
+                const bool has_si = prim >= 0;
+                if (COUNT) {
+                    ++c_traced;
+                    c_surf += has_si ? 1u : 0u;
+                    c_light += has_li ? 1u : 0u;
+                }
+                if (has_si) si_pos = ro + rd * t;
+                if (has_li && (!has_si || length(si_pos - ro) > length(li_pos - ro))) {
+                    cv = isfinite_(li_pow) ? li_pow : 1.0f;
+                } else if (!has_si) {
+                    cv = 0.0f;
+                } else {
+                    if (COUNT) ++c_exp;
+                    const int nchild = kp.n_rays >> rdepth;
+                    if (nchild == 0) {
+                        const float zero = 0.0f;
+                        cv = zero / (float)nchild;  // 0/0: the NaN that poisons the parent
+                    } else {
+                        push = true;
+                    }
+                }
+            }
+            if (push) {
+                if (is_iter) {
+                    float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
+                    b[0 * kBlock] = tpos.x; b[1 * kBlock] = tpos.y; b[2 * kBlock] = tpos.z;
+                    b[3 * kBlock] = tfr.m0.x; b[4 * kBlock] = tfr.m0.y; b[5 * kBlock] = tfr.m0.z;
+                    b[6 * kBlock] = tfr.m1.x; b[7 * kBlock] = tfr.m1.y; b[8 * kBlock] = tfr.m1.z;
+                    b[9 * kBlock] = tfr.m2.x; b[10 * kBlock] = tfr.m2.y; b[11 * kBlock] = tfr.m2.z;
+                    b[12 * kBlock] = tfr.iz.x; b[13 * kBlock] = tfr.iz.y; b[14 * kBlock] = tfr.iz.z;
+                    b[15 * kBlock] = tres;
+                    b[16 * kBlock] = mult;
+                    b[17 * kBlock] = __int_as_float(ti);
+                }
+                tpos = si_pos;
+                if (prim < 5) {
+                    const float* f = wallf + prim * 12;
+                    tfr.m0 = v3(f[0], f[1], f[2]);
+                    tfr.m1 = v3(f[3], f[4], f[5]);
+                    tfr.m2 = v3(f[6], f[7], f[8]);
+                    tfr.iz = v3(f[9], f[10], f[11]);
+                } else {
+                    const vec3 nrm = prim == 5 ? normalize(si_pos) : normalize(si_pos - sph_c);
+                    tfr = make_frame(nrm);
+                    if (COUNT) ++c_sframe;
+                }
+                tres = 0.0f;
+                ti = 0;
+                tdepth = rdepth;
+            } else if (is_iter) {
+                tres = tres + (mult * 1.0f) * cv;
+            } else {
+                // the camera ray itself ended (light, miss, depth_max or n_rays==0)
+                const float val = cv >= 0.0f ? cv : 0.0f;
+                kp.values[unit] = val;
+                has_path = false;
+            }
+        }
+    }
+
+    if (COUNT) {
+        atomicAdd(&kp.counters[0], (unsigned long long)c_paths);
+        atomicAdd(&kp.counters[1], (unsigned long long)c_traced);
+        atomicAdd(&kp.counters[2], (unsigned long long)c_surf);
+        atomicAdd(&kp.counters[3], (unsigned long long)c_light);
+        atomicAdd(&kp.counters[4], (unsigned long long)c_exp);
+        atomicAdd(&kp.counters[5], (unsigned long long)c_iter);
+        atomicAdd(&kp.counters[6], (unsigned long long)c_lsamp);
+        atomicAdd(&kp.counters[7], (unsigned long long)c_skip);
+        atomicAdd(&kp.counters[8], (unsigned long long)c_sframe);
+        atomicAdd(&kp.counters[9], (unsigned long long)c_ltr);
+        atomicAdd(&kp.counters[10], (unsigned long long)c_drift);
+    }
+}
+
+struct AParams {
+    int W, H, spp, n_cand;
+    const int* cand_of_row;  // [H] candidate index or -1
+    const float* values;
+    const uint8_t* codes;
+    const uint8_t* flags;
+    int tile_rows, n_shards, shard_id;
+    float* pixels;
+    uint32_t* counters;
+    float* sums;
+    float* pixel_max;
+};
+
+__device__ __forceinline__ void add_ray(float v, float& p, uint32_t& c, float& s, float& m) {
+    // GridRenderPlane::addRay (GridRenderPlane.cpp:68-73)
+    p = (p * (float)c + v) / (float)(c + 1u);
+    ++c;
+    s += v;
+    if (p > m) m = p;
+}
+
+__global__ __launch_bounds__(256) void accumulate_kernel(AParams ap) {
+    const int xi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int yi = blockIdx.y;
+    if (xi >= ap.W) return;
+    if (!(ap.n_shards <= 1 || ap.tile_rows <= 0 || ((yi / ap.tile_rows) % ap.n_shards) == ap.shard_id))
+        return;
+    const size_t d = (size_t)yi * ap.W + xi;
+    float p = ap.pixels[d];
+    uint32_t c = ap.counters[d];
+    float s = ap.sums ? ap.sums[d] : 0.0f;
+    float m = ap.pixel_max ? ap.pixel_max[d] : 0.0f;
+    const size_t pass_stride = (size_t)ap.n_cand * ap.W;
+    const int H = ap.H;
+    if (ap.flags[d] == 0) {
+        // nominal sources only: source row H-2-yi (and H-1 for yi == 0)
+        int r0 = H - 2 - yi;
+        const int c0 = r0 >= 0 ? ap.cand_of_row[r0] : -1;
+        const int c1 = (yi == 0 && H >= 1) ? ap.cand_of_row[H - 1] : -1;
+        for (int sp = 0; sp < ap.spp; ++sp) {
+            const size_t base = (size_t)sp * pass_stride;
+            if (c0 >= 0) add_ray(ap.values[base + (size_t)c0 * ap.W + xi], p, c, s, m);
+            if (c1 >= 0 && c1 != c0) add_ray(ap.values[base + (size_t)c1 * ap.W + xi], p, c, s, m);
+        }
+    } else {
+        int rows[4];
+        int nr = 0;
+        const int cand_rows[4] = {H - 3 - yi, H - 2 - yi, H - 1 - yi, yi <= 1 ? H - 1 : -1};
+        for (int q = 0; q < 4; ++q) {
+            const int r = cand_rows[q];
+            if (r < 0 || r >= H) continue;
+            bool dup = false;
+            for (int e = 0; e < nr; ++e) dup |= rows[e] == r;
+            if (!dup) rows[nr++] = r;
+        }
+        // ascending row order (raster order of render_sample)
+        for (int a = 0; a < nr; ++a)
+            for (int b2 = a + 1; b2 < nr; ++b2)
+                if (rows[b2] < rows[a]) { int t = rows[a]; rows[a] = rows[b2]; rows[b2] = t; }
+        for (int sp = 0; sp < ap.spp; ++sp) {
+            const size_t base = (size_t)sp * pass_stride;
+            for (int a = 0; a < nr; ++a) {
+                const int iy = rows[a];
+                const int ci = ap.cand_of_row[iy];
+                if (ci < 0) continue;
+                const int yn = H - 2 - iy > 0 ? H - 2 - iy : 0;
+                for (int ix = xi - 1; ix <= xi + 1; ++ix) {
+                    if (ix < 0 || ix >= ap.W) continue;
+                    const size_t idx = base + (size_t)ci * ap.W + ix;
+                    const uint8_t code = ap.codes[idx];
+                    if (code >= 0x10) continue;
+                    const int dx = (code & 3) - 1, dy = ((code >> 2) & 3) - 1;
+                    if (ix + dx == xi && yn + dy == yi) add_ray(ap.values[idx], p, c, s, m);
+                }
+            }
+        }
+    }
+    ap.pixels[d] = p;
+    ap.counters[d] = c;
+    if (ap.sums) ap.sums[d] = s;
+    if (ap.pixel_max) ap.pixel_max[d] = m;
+}
+
+// ----------------------------------------------------------- math probes
+__device__ __host__ inline float math_fn(int fn, float x) {
+    switch (fn) {
+        case 0: return acosf_(x);
+        case 1: return sinf_(x);
+        case 2: return cosf_(x);
+        case 3: return acos_f64_to_f32(x);
+        case 4: { float s, c; sincosf_(x, &s, &c); return s; }
+        case 5: { float s, c; sincosf_(x, &s, &c); return c; }
+        case 6: return sqrt_(x);
+        case 7: return div_pi_to_f32(x);
+        case 8: return two_pi_times(x);
+        default: return 0.0f;
+    }
+}
+__global__ void math_kernel(int fn, const float* in, float* out, long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = math_fn(fn, in[i]);
+}
+
+// ---------------------------------------------------------------- context
+std::mutex g_err_mu;
+std::string g_err_global;
+
+}  // namespace
+
+struct ipt_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool has_scene = false;
+    int geometry_kind = 0;
+    int n_lights = 0;
+    LightDev* d_lights = nullptr;
+    float* d_weights = nullptr;
+    float* d_cdf = nullptr;
+    Frame* d_wall = nullptr;
+    float4* d_spheres = nullptr;
+    int n_spheres = 0;
+    vec3 cam_pos, cam_dir, cam_right, cam_up;
+    // work buffers
+    float* d_values = nullptr;
+    uint8_t* d_codes = nullptr;
+    size_t work_cap = 0;  // elements
+    uint8_t* d_flags = nullptr;
+    size_t flags_cap = 0;
+    int* d_cand_rows = nullptr;
+    int* d_cand_of_row = nullptr;
+    int cand_cap_rows = 0, cand_cap_h = 0;
+    unsigned long long* d_unit = nullptr;
+    unsigned long long* d_counters = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_path_ms = 0.0f, last_acc_ms = 0.0f;
+};
+
+namespace {
+
+int fail(ipt_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) {
+        ctx->err = msg;
+    } else {
+        std::lock_guard<std::mutex> g(g_err_mu);
+        g_err_global = msg;
+    }
+    return code;
+}
+#define HIPCHECK(ctx, expr)                                                             \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(ctx, IPT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int ensure_work(ipt_ctx* ctx, size_t elems, size_t npix, int H, int n_cand) {
+    if (elems > ctx->work_cap) {
+        if (ctx->d_values) hipFree(ctx->d_values);
+        if (ctx->d_codes) hipFree(ctx->d_codes);
+        ctx->d_values = nullptr;
+        ctx->d_codes = nullptr;
+        HIPCHECK(ctx, hipMalloc(&ctx->d_values, elems * sizeof(float)));
+        HIPCHECK(ctx, hipMalloc(&ctx->d_codes, elems));
+        ctx->work_cap = elems;
+    }
+    if (npix > ctx->flags_cap) {
+        if (ctx->d_flags) hipFree(ctx->d_flags);
+        ctx->d_flags = nullptr;
+        HIPCHECK(ctx, hipMalloc(&ctx->d_flags, npix));
+        ctx->flags_cap = npix;
+    }
+    if (n_cand > ctx->cand_cap_rows || H > ctx->cand_cap_h) {
+        if (ctx->d_cand_rows) hipFree(ctx->d_cand_rows);
+        if (ctx->d_cand_of_row) hipFree(ctx->d_cand_of_row);
+        ctx->d_cand_rows = nullptr;
+        ctx->d_cand_of_row = nullptr;
+        HIPCHECK(ctx, hipMalloc(&ctx->d_cand_rows, sizeof(int) * std::max(n_cand, 1)));
+        HIPCHECK(ctx, hipMalloc(&ctx->d_cand_of_row, sizeof(int) * std::max(H, 1)));
+        ctx->cand_cap_rows = n_cand;
+        ctx->cand_cap_h = H;
+    }
+    return IPT_OK;
+}
+
+bool owned_host(const ipt_params* p, int yi) {
+    if (p->n_shards <= 1 || p->tile_rows <= 0) return true;
+    return ((yi / p->tile_rows) % p->n_shards) == p->shard_id;
+}
+
+// Source rows whose samples can land in an owned destination row:
+// nominal row H-2-iy (0 for iy=H-1) within +-1 of an owned row.
+void candidate_rows(const ipt_params* p, std::vector<int>& rows, std::vector<int>& of_row) {
+    const int H = p->height;
+    rows.clear();
+    of_row.assign(H, -1);
+    for (int iy = 0; iy < H; ++iy) {
+        const int yn = H - 2 - iy > 0 ? H - 2 - iy : 0;
+        bool c = false;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int y = yn + dy;
+            if (y >= 0 && y < H && owned_host(p, y)) c = true;
+        }
+        if (c) {
+            of_row[iy] = (int)rows.size();
+            rows.push_back(iy);
+        }
+    }
+}
+
+int validate(ipt_ctx* ctx, const ipt_params* p) {
+    if (!ctx) return IPT_E_INVALID;
+    if (!p) return fail(ctx, IPT_E_INVALID, "params is NULL");
+    if (!ctx->has_scene) return fail(ctx, IPT_E_NOSCENE, "no scene uploaded");
+    if (p->width <= 0 || p->height <= 0 || p->width > 65536 || p->height > 65536)
+        return fail(ctx, IPT_E_INVALID, "width/height out of range");
+    if ((int64_t)p->width * p->height > (int64_t)1 << 31)
+        return fail(ctx, IPT_E_INVALID, "frame larger than 2^31 pixels");
+    if (p->spp < 0 || p->spp_offset < 0) return fail(ctx, IPT_E_INVALID, "negative spp");
+    if (p->n_rays < 0 || p->n_rays > 64) return fail(ctx, IPT_E_UNSUPPORTED, "n_rays must be in [0,64]");
+    if (p->depth_max < 0 || p->depth_max > 64) return fail(ctx, IPT_E_INVALID, "depth_max out of range");
+    if (p->n_shards > 1 && (p->shard_id < 0 || p->shard_id >= p->n_shards))
+        return fail(ctx, IPT_E_INVALID, "shard_id out of range");
+    return IPT_OK;
+}
+
+// Number of suspended stack levels the DFS can need.
+int needed_susp(const ipt_params* p) {
+    // a node at depth d is pushed iff d < depth_max and (n_rays >> d) > 0
+    int maxpush = -1;
+    for (int d = 0; d < p->depth_max; ++d)
+        if ((p->n_rays >> d) > 0) maxpush = d;
+    return maxpush < 0 ? 0 : maxpush;  // suspended levels = depth of deepest pushed node
+}
+
+template <int MAXSUSP>
+int launch_path(ipt_ctx* ctx, const KParams& kp, hipStream_t st, bool count) {
+    const size_t lds = (size_t)MAXSUSP * kStackFields * kBlock * sizeof(float) + 60 * sizeof(float);
+    const int blocks_per_cu = lds * 2 <= 160 * 1024 ? 2 : 1;
+    dim3 grid(ctx->n_cu * blocks_per_cu), block(kBlock);
+    HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (count)
+        hipLaunchKernelGGL((path_kernel<MAXSUSP, true>), grid, block, lds, st, kp);
+    else
+        hipLaunchKernelGGL((path_kernel<MAXSUSP, false>), grid, block, lds, st, kp);
+    HIPCHECK(ctx, hipGetLastError());
+    return IPT_OK;
+}
+
+int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t st,
+                  float* host_values, uint8_t* host_codes) {
+    std::vector<int> rows, of_row;
+    candidate_rows(p, rows, of_row);
+    const int n_cand = (int)rows.size();
+    const int W = p->width, H = p->height;
+    const size_t per_pass = (size_t)n_cand * W;
+    if (per_pass == 0 || p->spp == 0) return IPT_OK;
+    // chunk passes so the radiance buffer stays <= 1 GiB of floats
+    const size_t budget = (size_t)1 << 28;
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->spp, budget / per_pass));
+    if (host_values) chunk = p->spp;  // debug path: one chunk
+    int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
+    if (rc) return rc;
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice, st));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice, st));
+    const int susp = needed_susp(p);
+    const bool count = (p->flags & IPT_FLAG_COUNTERS) != 0;
+    float path_ms = 0.0f, acc_ms = 0.0f;
+    for (int s0 = 0; s0 < p->spp; s0 += chunk) {
+        const int ns = std::min(chunk, p->spp - s0);
+        KParams kp{};
+        kp.W = W;
+        kp.H = H;
+        kp.spp = ns;
+        kp.spp_offset = p->spp_offset + s0;
+        kp.n_rays = p->n_rays;
+        kp.depth_max = p->depth_max;
+        kp.key0 = (uint32_t)p->seed;
+        kp.key1 = (uint32_t)(p->seed >> 32);
+        kp.n_cand = n_cand;
+        kp.cand_rows = ctx->d_cand_rows;
+        kp.tile_rows = p->tile_rows;
+        kp.n_shards = p->n_shards;
+        kp.shard_id = p->shard_id;
+        kp.total_units = (unsigned long long)ns * per_pass;
+        kp.unit_counter = ctx->d_unit;
+        kp.values = ctx->d_values;
+        kp.codes = ctx->d_codes;
+        kp.flags = ctx->d_flags;
+        kp.counters = ctx->d_counters;
+        kp.geometry_kind = ctx->geometry_kind;
+        kp.n_lights = ctx->n_lights;
+        kp.lights = ctx->d_lights;
+        kp.weights = ctx->d_weights;
+        kp.cdf = ctx->d_cdf;
+        kp.wall_frames = ctx->d_wall;
+        kp.cam_pos = ctx->cam_pos;
+        kp.cam_dir = ctx->cam_dir;
+        kp.cam_right = ctx->cam_right;
+        kp.cam_up = ctx->cam_up;
+        kp.n_spheres = ctx->n_spheres;
+        kp.spheres = ctx->d_spheres;
+        HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
+        HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
+        if (susp <= 4)
+            rc = launch_path<4>(ctx, kp, st, count);
+        else if (susp <= 6)
+            rc = launch_path<6>(ctx, kp, st, count);
+        else if (susp <= 8)
+            rc = launch_path<8>(ctx, kp, st, count);
+        else
+            return fail(ctx, IPT_E_UNSUPPORTED, "recursion deeper than 8 suspended levels");
+        if (rc) return rc;
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[1], st));
+        if (img) {
+            AParams ap{};
+            ap.W = W;
+            ap.H = H;
+            ap.spp = ns;
+            ap.n_cand = n_cand;
+            ap.cand_of_row = ctx->d_cand_of_row;
+            ap.values = ctx->d_values;
+            ap.codes = ctx->d_codes;
+            ap.flags = ctx->d_flags;
+            ap.tile_rows = p->tile_rows;
+            ap.n_shards = p->n_shards;
+            ap.shard_id = p->shard_id;
+            ap.pixels = img->pixels;
+            ap.counters = img->counters;
+            ap.sums = img->sums;
+            ap.pixel_max = img->pixel_max;
+            dim3 grid((W + 255) / 256, H), block(256);
+            hipLaunchKernelGGL(accumulate_kernel, grid, block, 0, st, ap);
+            HIPCHECK(ctx, hipGetLastError());
+        }
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[2], st));
+        if (host_values) {
+            HIPCHECK(ctx, hipMemcpyAsync(host_values, ctx->d_values, sizeof(float) * ns * per_pass, hipMemcpyDeviceToHost, st));
+            HIPCHECK(ctx, hipMemcpyAsync(host_codes, ctx->d_codes, ns * per_pass, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHECK(ctx, hipEventSynchronize(ctx->ev[2]));
+        float a = 0, b = 0;
+        HIPCHECK(ctx, hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
+        HIPCHECK(ctx, hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]));
+        path_ms += a;
+        acc_ms += b;
+    }
+    ctx->last_path_ms = path_ms;
+    ctx->last_acc_ms = acc_ms;
+    return IPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ipt_abi_version(void) { return IPT_ABI_VERSION; }
+
+const char* ipt_last_error(ipt_ctx* ctx) {
+    if (ctx) return ctx->err.c_str();
+    std::lock_guard<std::mutex> g(g_err_mu);
+    return g_err_global.c_str();
+}
+
+int ipt_create(int hip_device, ipt_ctx** out) {
+    if (!out) return fail(nullptr, IPT_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(nullptr, IPT_E_DEVICE, "no HIP device available (the path tracer has no CPU fallback)");
+    if (hip_device < 0 || hip_device >= n) return fail(nullptr, IPT_E_INVALID, "bad device index");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) != hipSuccess)
+        return fail(nullptr, IPT_E_DEVICE, "hipGetDeviceProperties failed");
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+        return fail(nullptr, IPT_E_DEVICE, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950 only");
+    ipt_ctx* ctx = new ipt_ctx();
+    ctx->device = hip_device;
+    ctx->n_cu = prop.multiProcessorCount;
+    if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return fail(nullptr, IPT_E_DEVICE, "stream creation failed");
+    }
+    for (auto& e : ctx->ev) hipEventCreate(&e);
+    if (hipMalloc(&ctx->d_unit, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * kNumCounters) != hipSuccess ||
+        hipMalloc(&ctx->d_wall, sizeof(Frame) * 5) != hipSuccess) {
+        ipt_destroy(ctx);
+        return fail(nullptr, IPT_E_OOM, "hipMalloc failed");
+    }
+    hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * kNumCounters);
+    *out = ctx;
+    return IPT_OK;
+}
+
+void ipt_destroy(ipt_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    void* bufs[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
+                    ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
+                    ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters};
+    for (void* b : bufs)
+        if (b) hipFree(b);
+    for (auto& e : ctx->ev)
+        if (e) hipEventDestroy(e);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
+    if (!ctx) return IPT_E_INVALID;
+    if (!s) return fail(ctx, IPT_E_INVALID, "scene is NULL");
+    if (s->geometry_kind != IPT_GEOM_SPHERE_IN_BOX && s->geometry_kind != IPT_GEOM_SPHERES_IN_BOX)
+        return fail(ctx, IPT_E_UNSUPPORTED, "unknown geometry_kind");
+    if (s->n_lights < 0 || s->n_lights > kMaxLights || (s->n_lights > 0 && !s->lights))
+        return fail(ctx, IPT_E_UNSUPPORTED, "n_lights out of range");
+    if (s->n_spheres < 0 || (s->n_spheres > 0 && !s->spheres))
+        return fail(ctx, IPT_E_INVALID, "bad sphere array");
+    hipSetDevice(ctx->device);
+    const int nl = s->n_lights;
+    std::vector<LightDev> L(std::max(nl, 1));
+    std::vector<float> powers(std::max(nl, 1));
+    for (int i = 0; i < nl; ++i) {
+        const ipt_area_light& a = s->lights[i];
+        if (a.type != IPT_LIGHT_AREA_DIAMOND && a.type != IPT_LIGHT_AREA_TRIANGLE)
+            return fail(ctx, IPT_E_UNSUPPORTED, "unknown light type");
+        L[i] = make_light(v3(a.position[0], a.position[1], a.position[2]),
+                          v3(a.x_axis[0], a.x_axis[1], a.x_axis[2]),
+                          v3(a.y_axis[0], a.y_axis[1], a.y_axis[2]), a.power, a.type);
+        powers[i] = a.power;
+    }
+    std::vector<float> wts(nl + 1), cdf(nl + 1);
+    mixture_weights(powers.data(), nl, wts.data());
+    float acc = 0.0f;
+    for (int i = 0; i <= nl; ++i) {
+        acc += wts[i];  // UnionDdf::sample's running sum (ddf.cpp:145-146)
+        cdf[i] = acc;
+    }
+    // wall frames: RotateDdf(CosineDdf, -plane) for planes {+x,+y,+z,-x,-z}
+    const vec3 planes[5] = {v3(1, 0, 0), v3(0, 1, 0), v3(0, 0, 1), v3(-1, 0, 0), v3(0, 0, -1)};
+    Frame wall[5];
+    for (int i = 0; i < 5; ++i) wall[i] = make_frame(-planes[i]);
+    std::vector<float4> sph(std::max(s->n_spheres, 1));
+    for (int i = 0; i < s->n_spheres; ++i)
+        sph[i] = make_float4(s->spheres[i].center[0], s->spheres[i].center[1], s->spheres[i].center[2], s->spheres[i].radius);
+    void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres};
+    for (void* b : old)
+        if (b) hipFree(b);
+    ctx->d_lights = nullptr;
+    ctx->d_weights = ctx->d_cdf = nullptr;
+    ctx->d_spheres = nullptr;
+    HIPCHECK(ctx, hipMalloc(&ctx->d_lights, sizeof(LightDev) * L.size()));
+    HIPCHECK(ctx, hipMalloc(&ctx->d_weights, sizeof(float) * (nl + 1)));
+    HIPCHECK(ctx, hipMalloc(&ctx->d_cdf, sizeof(float) * (nl + 1)));
+    HIPCHECK(ctx, hipMalloc(&ctx->d_spheres, sizeof(float4) * sph.size()));
+    HIPCHECK(ctx, hipMemcpy(ctx->d_lights, L.data(), sizeof(LightDev) * L.size(), hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(ctx->d_weights, wts.data(), sizeof(float) * (nl + 1), hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(ctx->d_cdf, cdf.data(), sizeof(float) * (nl + 1), hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(ctx->d_wall, wall, sizeof(Frame) * 5, hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(ctx->d_spheres, sph.data(), sizeof(float4) * sph.size(), hipMemcpyHostToDevice));
+    ctx->geometry_kind = s->geometry_kind;
+    ctx->n_lights = nl;
+    ctx->n_spheres = s->n_spheres;
+    const ipt_camera& c = s->camera;
+    ctx->cam_pos = v3(c.position[0], c.position[1], c.position[2]);
+    ctx->cam_dir = v3(c.direction[0], c.direction[1], c.direction[2]);
+    ctx->cam_right = v3(c.right[0], c.right[1], c.right[2]);
+    ctx->cam_up = v3(c.up[0], c.up[1], c.up[2]);
+    ctx->has_scene = true;
+    return IPT_OK;
+}
+
+int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, void* hip_stream) {
+    int rc = validate(ctx, p);
+    if (rc) return rc;
+    if (!img || !img->pixels || !img->counters) return fail(ctx, IPT_E_INVALID, "image pixels/counters are NULL");
+    hipSetDevice(ctx->device);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    return render_chunks(ctx, p, img, st, nullptr, nullptr);
+}
+
+int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* himg) {
+    int rc = validate(ctx, p);
+    if (rc) return rc;
+    if (!himg || !himg->pixels || !himg->counters) return fail(ctx, IPT_E_INVALID, "image pixels/counters are NULL");
+    hipSetDevice(ctx->device);
+    const size_t npix = (size_t)p->width * p->height;
+    ipt_image d{};
+    HIPCHECK(ctx, hipMalloc(&d.pixels, npix * 4));
+    HIPCHECK(ctx, hipMalloc(&d.counters, npix * 4));
+    if (himg->sums) HIPCHECK(ctx, hipMalloc(&d.sums, npix * 4));
+    if (himg->pixel_max) HIPCHECK(ctx, hipMalloc(&d.pixel_max, npix * 4));
+    hipStream_t st = ctx->stream;
+    HIPCHECK(ctx, hipMemcpyAsync(d.pixels, himg->pixels, npix * 4, hipMemcpyHostToDevice, st));
+    HIPCHECK(ctx, hipMemcpyAsync(d.counters, himg->counters, npix * 4, hipMemcpyHostToDevice, st));
+    if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(d.sums, himg->sums, npix * 4, hipMemcpyHostToDevice, st));
+    if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(d.pixel_max, himg->pixel_max, npix * 4, hipMemcpyHostToDevice, st));
+    rc = render_chunks(ctx, p, &d, st, nullptr, nullptr);
+    if (rc == IPT_OK) {
+        HIPCHECK(ctx, hipMemcpyAsync(himg->pixels, d.pixels, npix * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(ctx, hipMemcpyAsync(himg->counters, d.counters, npix * 4, hipMemcpyDeviceToHost, st));
+        if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(himg->sums, d.sums, npix * 4, hipMemcpyDeviceToHost, st));
+        if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(himg->pixel_max, d.pixel_max, npix * 4, hipMemcpyDeviceToHost, st));
+        HIPCHECK(ctx, hipStreamSynchronize(st));
+    }
+    hipFree(d.pixels);
+    hipFree(d.counters);
+    if (d.sums) hipFree(d.sums);
+    if (d.pixel_max) hipFree(d.pixel_max);
+    return rc;
+}
+
+int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t* codes) {
+    int rc = validate(ctx, p);
+    if (rc) return rc;
+    if (!values || !codes) return fail(ctx, IPT_E_INVALID, "values/codes are NULL");
+    if (p->n_shards > 1) return fail(ctx, IPT_E_UNSUPPORTED, "ipt_render_values renders whole frames");
+    hipSetDevice(ctx->device);
+    rc = render_chunks(ctx, p, nullptr, ctx->stream, values, codes);
+    if (rc) return rc;
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return IPT_OK;
+}
+
+int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
+    if (!ctx || !out) return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    unsigned long long h[kNumCounters];
+    HIPCHECK(ctx, hipMemcpy(h, ctx->d_counters, sizeof h, hipMemcpyDeviceToHost));
+    out->paths = h[0];
+    out->traced_rays = h[1];
+    out->surface_hits = h[2];
+    out->light_hits = h[3];
+    out->expanded_nodes = h[4];
+    out->iterations = h[5];
+    out->light_samples = h[6];
+    out->skipped = h[7];
+    out->sphere_frames = h[8];
+    out->light_traces = h[9];
+    out->drifted = h[10];
+    return IPT_OK;
+}
+
+int ipt_reset_counters(ipt_ctx* ctx) {
+    if (!ctx) return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    HIPCHECK(ctx, hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * kNumCounters));
+    return IPT_OK;
+}
+
+int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms) {
+    if (!ctx) return IPT_E_INVALID;
+    if (path_ms) *path_ms = ctx->last_path_ms;
+    if (accumulate_ms) *accumulate_ms = ctx->last_acc_ms;
+    return IPT_OK;
+}
+
+int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
+    if (!in || !out || n < 0 || fn < 0 || fn > 8) return IPT_E_INVALID;
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([=]() {
+            for (int64_t i = t; i < n; i += nt) out[i] = math_fn(fn, in[i]);
+        });
+    for (auto& x : th) x.join();
+    return IPT_OK;
+}
+
+int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n) {
+    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 8) return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    float *din = nullptr, *dout = nullptr;
+    HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * 4));
+    HIPCHECK(ctx, hipMalloc(&dout, std::max<int64_t>(n, 1) * 4));
+    HIPCHECK(ctx, hipMemcpy(din, in, n * 4, hipMemcpyHostToDevice));
+    const long long blocks = (n + 255) / 256;
+    if (blocks > 0) hipLaunchKernelGGL(math_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, fn, din, dout, (long long)n);
+    HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHECK(ctx, hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost));
+    hipFree(din);
+    hipFree(dout);
+    return IPT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,447 @@
+// ipt_math.h — portable, bit-reproducible arithmetic for the ipt path tracer.
+//
+// Compiled by hipcc for BOTH the gfx950 device code and the host side of the
+// product library (same source, same operation order, -ffp-contract=off), so
+// a value computed on the GPU is bit-identical to the value the host side of
+// the library computes for the exhaustive math tests.
+//
+// What it reproduces:
+//  * glm 0.9.9.7 vec3/mat3 arithmetic in glm's operation order
+//    (reference include/glm/detail/func_geometric.inl:8-90,
+//     detail/type_mat3x3.inl:468-474, detail/func_matrix.inl:268-291,
+//     ext/matrix_transform.inl:18-47).
+//  * the libm functions the reference calls on its hot path, as shipped in the
+//    image's glibc 2.35 (x86_64, FMA/AVX2 ifunc variants that the reference
+//    binary binds to on any FMA-capable host):
+//      acosf  -> fdlibm __ieee754_acosf   (float ops, no FMA)
+//      sinf/cosf/sincosf -> ARM optimized-routines sinf/cosf (__sinf_fma,
+//                 __cosf_fma: double-precision polynomial, FMA-contracted
+//                 exactly where GCC contracted glibc's source)
+//      (float)acos((double)x) -> fdlibm __ieee754_acos restated in double;
+//                 only its rounding to float is used by the reference
+//                 (libddf/ddf_detail.h:82) and that rounding is verified equal
+//                 to glibc's for every float input in tests/.
+//    Constants were read from the image's libm.so.6 .rodata and the operation
+//    graphs from its disassembly; tests/test_math_exhaustive.py checks every
+//    float input of each function's reachable domain against the host libm.
+#pragma once
+
+#include <stdint.h>
+
+#ifndef IPT_HD
+#define IPT_HD __host__ __device__ inline
+#endif
+
+namespace ipt {
+
+// ---------------------------------------------------------------- bit casts
+IPT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+IPT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+IPT_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
+IPT_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
+
+IPT_HD float fabs_(float x) { return u2f(f2u(x) & 0x7fffffffu); }
+IPT_HD bool isfinite_(float x) { return (f2u(x) & 0x7f800000u) != 0x7f800000u; }
+IPT_HD float inf_() { return u2f(0x7f800000u); }
+IPT_HD double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+IPT_HD float sqrt_(float x) { return __builtin_sqrtf(x); }
+IPT_HD double sqrtd_(double x) { return __builtin_sqrt(x); }
+
+// ------------------------------------------------------------------ vec3
+// glm::vec3 with glm's component-wise operators; no FMA anywhere.
+struct vec3 {
+    float x, y, z;
+};
+IPT_HD vec3 v3(float x, float y, float z) { vec3 r; r.x = x; r.y = y; r.z = z; return r; }
+IPT_HD vec3 operator+(vec3 a, vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+IPT_HD vec3 operator-(vec3 a, vec3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+IPT_HD vec3 operator-(vec3 a) { return v3(-a.x, -a.y, -a.z); }
+IPT_HD vec3 operator*(vec3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+IPT_HD vec3 operator*(float s, vec3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+IPT_HD bool is_zero(vec3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+// glm compute_dot<vec3>: tmp = a*b; tmp.x + tmp.y + tmp.z   (func_geometric.inl:48-55)
+IPT_HD float dot(vec3 a, vec3 b) {
+    float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
+    return (tx + ty) + tz;
+}
+// glm compute_cross (func_geometric.inl:68-79)
+IPT_HD vec3 cross(vec3 x, vec3 y) {
+    return v3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+// glm length = sqrt(dot(v,v)) (func_geometric.inl:8-14)
+IPT_HD float length(vec3 v) { return sqrt_(dot(v, v)); }
+// glm normalize = v * inversesqrt(dot(v,v)), inversesqrt = 1/sqrt (func_exponential.inl:136-139)
+IPT_HD vec3 normalize(vec3 v) {
+    float s = 1.0f / sqrt_(dot(v, v));
+    return v * s;
+}
+
+// column-major mat3, m[c][r] as glm
+struct mat3 {
+    vec3 c[3];
+};
+// glm mat3 * vec3 (type_mat3x3.inl:468-474): row i = (m0i*vx + m1i*vy) + m2i*vz
+IPT_HD vec3 mul(const mat3& m, vec3 v) {
+    return v3(m.c[0].x * v.x + m.c[1].x * v.y + m.c[2].x * v.z,
+              m.c[0].y * v.x + m.c[1].y * v.y + m.c[2].y * v.z,
+              m.c[0].z * v.x + m.c[1].z * v.y + m.c[2].z * v.z);
+}
+IPT_HD float el(const mat3& m, int c, int r) {
+    const vec3& v = m.c[c];
+    return r == 0 ? v.x : (r == 1 ? v.y : v.z);
+}
+// glm compute_inverse<3,3> (func_matrix.inl:268-291), cofactor / determinant
+IPT_HD mat3 inverse(const mat3& M) {
+    const float m00 = M.c[0].x, m01 = M.c[0].y, m02 = M.c[0].z;
+    const float m10 = M.c[1].x, m11 = M.c[1].y, m12 = M.c[1].z;
+    const float m20 = M.c[2].x, m21 = M.c[2].y, m22 = M.c[2].z;
+    float det = m00 * (m11 * m22 - m21 * m12);
+    det = det - m10 * (m01 * m22 - m21 * m02);
+    det = det + m20 * (m01 * m12 - m11 * m02);
+    // glm writes "+ m00*(..) - m10*(..) + m20*(..)"; unary + is exact
+    const float o = 1.0f / det;
+    mat3 I;
+    I.c[0].x = (m11 * m22 - m21 * m12) * o;
+    I.c[1].x = -(m10 * m22 - m20 * m12) * o;
+    I.c[2].x = (m10 * m21 - m20 * m11) * o;
+    I.c[0].y = -(m01 * m22 - m21 * m02) * o;
+    I.c[1].y = (m00 * m22 - m20 * m02) * o;
+    I.c[2].y = -(m00 * m21 - m20 * m01) * o;
+    I.c[0].z = (m01 * m12 - m11 * m02) * o;
+    I.c[1].z = -(m00 * m12 - m10 * m02) * o;
+    I.c[2].z = (m00 * m11 - m10 * m01) * o;
+    return I;
+}
+
+// ------------------------------------------------------------------ acosf
+// glibc 2.35 sysdeps/ieee754/flt-32/e_acosf.c (fdlibm), constants verified
+// against libm.so.6 .rodata (0x9c958..0x9c98c).
+IPT_HD float acosf_(float x) {
+    const float one = 1.0f;
+    const float pi = u2f(0x40490fdau);
+    const float pio2_hi = u2f(0x3fc90fdau);
+    const float pio2_lo = u2f(0x33a22168u);
+    const float two_pio2_lo = u2f(0x34222168u);  // (float)2.0*pio2_lo, folded by GCC
+    const float pS0 = u2f(0x3e2aaaabu), pS1 = -u2f(0x3ea6b090u), pS2 = u2f(0x3e4e0aa8u),
+                pS3 = -u2f(0x3d241146u), pS4 = u2f(0x3a4f7f04u), pS5 = u2f(0x3811ef08u);
+    const float qS1 = -u2f(0x4019d139u), qS2 = u2f(0x4001572du), qS3 = -u2f(0x3f303361u),
+                qS4 = u2f(0x3d9dc62eu);
+    const uint32_t hx = f2u(x);
+    const uint32_t ix = hx & 0x7fffffffu;
+    if (ix == 0x3f800000u) {
+        if ((int32_t)hx > 0) return 0.0f;
+        return pi + two_pio2_lo;
+    } else if (ix > 0x3f800000u) {
+        return (x - x) / (x - x);
+    }
+    if (ix < 0x3f000000u) {  // |x| < 0.5
+        if (ix <= 0x32800000u) return pio2_hi + pio2_lo;
+        float z = x * x;
+        float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        float r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    } else if ((int32_t)hx < 0) {  // x < -0.5
+        float z = (one + x) * 0.5f;
+        float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        float s = sqrt_(z);
+        float r = p / q;
+        float w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    } else {  // x > 0.5
+        float z = (one - x) * 0.5f;
+        float s = sqrt_(z);
+        float df = u2f(f2u(s) & 0xfffff000u);
+        float c = (z - df * df) / (s + df);
+        float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        float r = p / q;
+        float w = r * s + c;
+        return 2.0f * (df + w);
+    }
+}
+
+// ------------------------------------------------------------ sinf / cosf
+// ARM optimized-routines single-precision sin/cos as built into glibc 2.35
+// (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h) in its FMA ifunc
+// variant. Table __sincosf_table read from libm .rodata 0xb30c0.
+struct sincos_tab {
+    double c0, c1, s1, c2, s2, c3, s3, c4;
+};
+IPT_HD sincos_tab sincos_table(int which) {
+    sincos_tab t;
+    const double sg = which ? -1.0 : 1.0;
+    t.c0 = sg * 1.0;
+    t.c1 = sg * u2d(0xbfdffffffd0c621cull);
+    t.s1 = u2d(0xbfc555545995a603ull);
+    t.c2 = sg * u2d(0x3fa55553e1068f19ull);
+    t.s2 = u2d(0x3f81107605230bc4ull);
+    t.c3 = sg * u2d(0xbf56c087e89a359dull);
+    t.s3 = u2d(0xbf2994eb3774cf24ull);
+    t.c4 = sg * u2d(0x3ef99343027bf8c3ull);
+    return t;
+}
+IPT_HD double sincos_sign(int q) { return (q == 1 || q == 2) ? -1.0 : 1.0; }
+IPT_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ffu; }
+
+// sin polynomial on reduced x (n even) — __sinf_fma @7b359 / @7b2e0
+IPT_HD float sin_poly_(double x, double x2, const sincos_tab& p) {
+    double s1 = fma_(x2, p.s3, p.s2);
+    double x3 = x2 * x;
+    double x7 = x2 * x3;
+    double s = fma_(x3, p.s1, x);
+    return (float)fma_(s1, x7, s);
+}
+// cos polynomial on reduced x (n odd for sin) — __sinf_fma @7b388
+IPT_HD float cos_poly_(double x2, const sincos_tab& p) {
+    double x4 = x2 * x2;
+    double c1 = fma_(x2, p.c1, p.c0);
+    double c2 = fma_(x2, p.c4, p.c3);
+    double x6 = x2 * x4;
+    double c = fma_(x4, p.c2, c1);
+    return (float)fma_(c2, x6, c);
+}
+
+// reduce_large (sincosf.h) with __inv_pio4 (libm .rodata 0xb3060)
+IPT_HD double reduce_large_(uint32_t xi, int* np) {
+    const uint32_t inv_pio4[24] = {
+        0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
+        0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
+        0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
+        0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u};
+    const uint32_t* arr = &inv_pio4[(xi >> 26) & 15];
+    int shift = (xi >> 23) & 7;
+    uint64_t n, res0, res1, res2;
+    xi = (xi & 0xffffffu) | 0x800000u;
+    xi <<= shift;
+    res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+    res1 = (uint64_t)xi * arr[4];
+    res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    n = (res0 + (1ull << 61)) >> 62;
+    res0 -= n << 62;
+    double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * u2d(0x3c1921fb54442d18ull);  // pi * 2^-62
+}
+
+// fast reduction: n = round(x*2/pi) via (int)(x*hpi_inv*2^24) + 2^23 >> 24; x - n*hpi (one FMA)
+IPT_HD double reduce_fast_(double x, int* np) {
+    const double hpi_inv = u2d(0x41645f306dc9c883ull);  // 0x1.45f306dc9c883p+23
+    double r = x * hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return fma_(-(double)n, u2d(0x3ff921fb54442d18ull), x);
+}
+
+IPT_HD float sinf_(float y) {
+    double x = y;
+    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {  // pio4
+        double s = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return y;
+        return sin_poly_(x, s, sincos_table(0));
+    } else if (abstop12(y) < abstop12(120.0f)) {
+        int n;
+        x = reduce_fast_(x, &n);
+        double s = sincos_sign(n & 3);
+        sincos_tab p = sincos_table((n & 2) ? 1 : 0);
+        double x2 = x * x;
+        if ((n & 1) == 0) return sin_poly_(x * s, x2, p);
+        return cos_poly_(x2, p);
+    } else if (abstop12(y) < abstop12(u2f(0x7f800000u))) {
+        uint32_t xi = f2u(y);
+        int sign = xi >> 31;
+        int n;
+        x = reduce_large_(xi, &n);
+        double s = sincos_sign((n + sign) & 3);
+        sincos_tab p = sincos_table(((n + sign) & 2) ? 1 : 0);
+        double x2 = x * x;
+        if ((n & 1) == 0) return sin_poly_(x * s, x2, p);
+        return cos_poly_(x2, p);
+    }
+    return (y - y) / (y - y);
+}
+
+IPT_HD float cosf_(float y) {
+    double x = y;
+    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+        return cos_poly_(x2, sincos_table(0));
+    } else if (abstop12(y) < abstop12(120.0f)) {
+        int n;
+        x = reduce_fast_(x, &n);
+        double s = sincos_sign(n & 3);
+        sincos_tab p = sincos_table((n & 2) ? 1 : 0);
+        double x2 = x * x;
+        if (n & 1) return sin_poly_(x * s, x2, p);
+        return cos_poly_(x2, p);
+    } else if (abstop12(y) < abstop12(u2f(0x7f800000u))) {
+        uint32_t xi = f2u(y);
+        int sign = xi >> 31;
+        int n;
+        x = reduce_large_(xi, &n);
+        double s = sincos_sign((n + sign) & 3);
+        sincos_tab p = sincos_table(((n + sign) & 2) ? 1 : 0);
+        double x2 = x * x;
+        if (n & 1) return sin_poly_(x * s, x2, p);
+        return cos_poly_(x2, p);
+    }
+    return (y - y) / (y - y);
+}
+
+// sin and cos of the same argument sharing one reduction, for |y| < 120
+// (every argument the path tracer produces: rotation angles in [0,pi],
+// CosineDdf angles in [0,pi/2] and [0,2pi)). Equal bit-for-bit to
+// sinf_/cosf_ there (glibc's __sincosf_fma SLP-vectorises the same FMA graph;
+// tests/test_math_exhaustive.py checks the equality against host sincosf).
+IPT_HD void sincosf_small_(float y, float* sp, float* cp) {
+    double x = y;
+    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) { *sp = y; *cp = 1.0f; return; }
+        sincos_tab p = sincos_table(0);
+        *sp = sin_poly_(x, x2, p);
+        *cp = cos_poly_(x2, p);
+        return;
+    }
+    int n;
+    x = reduce_fast_(x, &n);
+    double s = sincos_sign(n & 3);
+    sincos_tab p = sincos_table((n & 2) ? 1 : 0);
+    double x2 = x * x;
+    float a = sin_poly_(x * s, x2, p);
+    float b = cos_poly_(x2, p);
+    if (n & 1) { *sp = b; *cp = a; } else { *sp = a; *cp = b; }
+}
+IPT_HD void sincosf_(float y, float* sp, float* cp) {
+    if (abstop12(y) < abstop12(120.0f)) {
+        sincosf_small_(y, sp, cp);
+        return;
+    }
+    *sp = sinf_(y);
+    *cp = cosf_(y);
+}
+// sinf for |y| < 120 (same code path as sinf_ there)
+IPT_HD float sinf_small_(float y) {
+    double x = y;
+    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {
+        double s = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return y;
+        return sin_poly_(x, s, sincos_table(0));
+    }
+    int n;
+    x = reduce_fast_(x, &n);
+    double s = sincos_sign(n & 3);
+    sincos_tab p = sincos_table((n & 2) ? 1 : 0);
+    double x2 = x * x;
+    if ((n & 1) == 0) return sin_poly_(x * s, x2, p);
+    return cos_poly_(x2, p);
+}
+
+// ------------------------------------------------- (float)acos((double)x)
+// fdlibm e_acos.c (double). Used only through its rounding to float; the
+// equality of that rounding with glibc's acos for all float inputs in [-1,1]
+// is checked exhaustively in tests/test_math_exhaustive.py.
+IPT_HD double acos_d_(double x) {
+    const double pi = u2d(0x400921fb54442d18ull);
+    const double pio2_hi = u2d(0x3ff921fb54442d18ull);
+    const double pio2_lo = u2d(0x3c91a62633145c07ull);
+    const double pS0 = u2d(0x3fc5555555555555ull), pS1 = u2d(0xbfd4d61203eb6f7dull),
+                 pS2 = u2d(0x3fc9c1550e884455ull), pS3 = u2d(0xbfa48228b5688f3bull),
+                 pS4 = u2d(0x3f49efe07501b288ull), pS5 = u2d(0x3f023de10dfdf709ull);
+    const double qS1 = u2d(0xc0033a271c8a2d4bull), qS2 = u2d(0x40002ae59c598ac8ull),
+                 qS3 = u2d(0xbfe6066c1b8d0159ull), qS4 = u2d(0x3fb3b8c5b12e9282ull);
+    const uint64_t hx64 = d2u(x);
+    const uint32_t hx = (uint32_t)(hx64 >> 32);
+    const uint32_t ix = hx & 0x7fffffffu;
+    if (ix >= 0x3ff00000u) {
+        if (((ix - 0x3ff00000u) | (uint32_t)hx64) == 0) {
+            if ((int32_t)hx > 0) return 0.0;
+            return pi + 2.0 * pio2_lo;
+        }
+        return (x - x) / (x - x);
+    }
+    if (ix < 0x3fe00000u) {
+        if (ix <= 0x3c600000u) return pio2_hi + pio2_lo;
+        double z = x * x;
+        double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        double r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    } else if ((int32_t)hx < 0) {
+        double z = (1.0 + x) * 0.5;
+        double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        double s = sqrtd_(z);
+        double r = p / q;
+        double w = r * s - pio2_lo;
+        return pi - 2.0 * (s + w);
+    } else {
+        double z = (1.0 - x) * 0.5;
+        double s = sqrtd_(z);
+        double df = u2d(d2u(s) & 0xffffffff00000000ull);
+        double c = (z - df * df) / (s + df);
+        double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        double r = p / q;
+        double w = r * s + c;
+        return 2.0 * (df + w);
+    }
+}
+IPT_HD float acos_f64_to_f32(float x) { return (float)acos_d_((double)x); }
+
+// --------------------------------------------------- mixed-precision helpers
+// The reference compares floats against the double literal 1e-6
+// (geometric_utils.cpp:14,23,45-48; lighting.cpp:116,120). For a float f,
+// (double)f < 1e-6 <=> f < 0x358637be (the smallest float above 1e-6 is
+// 0x358637be; float(1e-6) = 0x358637bd < 1e-6).
+IPT_HD bool lt_1em6(float f) { return f < u2f(0x358637beu); }
+
+// CosineDdf::value (ddf.cpp:232-238): (float)((double)z / M_PI)
+IPT_HD float div_pi_to_f32(float z) { return (float)((double)z / u2d(0x400921fb54442d18ull)); }
+
+// CosineDdf::sample phi (ddf.cpp:228): (float)(2*M_PI*(double)u2)
+IPT_HD float two_pi_times(float u) { return (float)(u2d(0x401921fb54442d18ull) * (double)u); }
+
+// ------------------------------------------------------------ RNG (Philox)
+// Philox4x32-10 (Salmon et al., SC'11; Random123 constants).
+struct u32x4 {
+    uint32_t v[4];
+};
+IPT_HD void mulhilo32(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    *hi = (uint32_t)(p >> 32);
+    *lo = (uint32_t)p;
+}
+IPT_HD u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                           uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0, lo0, hi1, lo1;
+        mulhilo32(M0, c0, &hi0, &lo0);
+        mulhilo32(M1, c2, &hi1, &lo1);
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += W0;
+        k1 += W1;
+    }
+    u32x4 out;
+    out.v[0] = c0;
+    out.v[1] = c1;
+    out.v[2] = c2;
+    out.v[3] = c3;
+    return out;
+}
+// uniform float in [0,1): top 24 bits * 2^-24 (never 1.0, so randf.h's retry
+// loop at include/randf.h:8-9 never fires)
+IPT_HD float u01(uint32_t w) { return (float)(w >> 8) * 5.9604644775390625e-08f; }
+
+}  // namespace ipt

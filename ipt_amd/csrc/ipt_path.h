@@ -1,0 +1,290 @@
+// ipt_path.h — per-ray building blocks of the reference estimator, restated
+// for the gfx950 megakernel (and compiled for the host side of the library,
+// which uses them to precompute scene constants with identical arithmetic).
+//
+// Every function cites the reference lines it reproduces. All arithmetic is
+// in the reference's order; the build uses -ffp-contract=off.
+#pragma once
+
+#include "ipt_math.h"
+
+namespace ipt {
+
+constexpr int kMaxLights = 1024;
+
+// ------------------------------------------------------------- scene (device)
+struct LightDev {
+    vec3 P;        // Light::position (corner)
+    vec3 x, y;     // x_axis, y_axis
+    vec3 n;        // normalize(cross(x_axis, y_axis))         lighting.cpp:126,141
+    mat3 inv;      // inverse(mat3(x, y, cross(x,y)))          lighting.cpp:87-89
+    float area;    // |cross| or |cross|/2                     lighting.cpp:84-85
+    float spow;    // power/area                               lighting.cpp:102,142
+    int type;      // 0 diamond, 1 triangle
+    int pad;
+};
+
+// Rotation frame of a RotateDdf(CosineDdf, to) (ddf_detail.h:72-85):
+// sample = M * x, value = CosineDdf::value(inverse * d) needs only row 2 of
+// the inverse.
+struct Frame {
+    vec3 m0, m1, m2;  // columns of M
+    vec3 iz;          // (inv[0][2], inv[1][2], inv[2][2])
+};
+
+// RotateDdf constructor (ddf_detail.h:73-84) incl. glm::rotate
+// (ext/matrix_transform.inl:18-47) applied to identity and mat3(mat4).
+IPT_HD Frame make_frame(vec3 to) {
+    const vec3 z = v3(0.0f, 0.0f, 1.0f);
+    vec3 axis = cross(z, to);
+    if (lt_1em6(length(axis))) axis = v3(1.0f, 0.0f, 0.0f);
+    const float cosinus = dot(z, to);
+    const float a = acos_f64_to_f32(cosinus);
+    float s, c;
+    sincosf_small_(a, &s, &c);  // glm::rotate's cos(a), sin(a); a in [0,pi]
+    const vec3 ax = normalize(axis);
+    const vec3 temp = (1.0f - c) * ax;
+    float R[3][3];
+    R[0][0] = c + temp.x * ax.x;
+    R[0][1] = temp.x * ax.y + s * ax.z;
+    R[0][2] = temp.x * ax.z - s * ax.y;
+    R[1][0] = temp.y * ax.x - s * ax.z;
+    R[1][1] = c + temp.y * ax.y;
+    R[1][2] = temp.y * ax.z + s * ax.x;
+    R[2][0] = temp.z * ax.x + s * ax.y;
+    R[2][1] = temp.z * ax.y - s * ax.x;
+    R[2][2] = c + temp.z * ax.z;
+    // Result[k] = m[0]*R[k][0] + m[1]*R[k][1] + m[2]*R[k][2] with m = identity(4)
+    mat3 M;
+    for (int k = 0; k < 3; ++k) {
+        float e0 = (1.0f * R[k][0] + 0.0f * R[k][1]) + 0.0f * R[k][2];
+        float e1 = (0.0f * R[k][0] + 1.0f * R[k][1]) + 0.0f * R[k][2];
+        float e2 = (0.0f * R[k][0] + 0.0f * R[k][1]) + 1.0f * R[k][2];
+        M.c[k] = v3(e0, e1, e2);
+    }
+    const mat3 I = inverse(M);
+    Frame f;
+    f.m0 = M.c[0];
+    f.m1 = M.c[1];
+    f.m2 = M.c[2];
+    f.iz = v3(I.c[0].z, I.c[1].z, I.c[2].z);
+    return f;
+}
+IPT_HD vec3 frame_apply(const Frame& f, vec3 v) {
+    return v3(f.m0.x * v.x + f.m1.x * v.y + f.m2.x * v.z,
+              f.m0.y * v.x + f.m1.y * v.y + f.m2.y * v.z,
+              f.m0.z * v.x + f.m1.z * v.y + f.m2.z * v.z);
+}
+// TransformDdf::value -> CosineDdf::value (ddf_detail.h:74-76, ddf.cpp:232-238)
+IPT_HD float frame_cosine_value(const Frame& f, vec3 d) {
+    const float z = f.iz.x * d.x + f.iz.y * d.y + f.iz.z * d.z;
+    if (z < 0.0f) return 0.0f;
+    return div_pi_to_f32(z);
+}
+
+// CosineDdf::sample (ddf.cpp:223-231) in local coordinates
+IPT_HD vec3 cosine_sample_local(float u1, float u2) {
+    const float cos_alpha = sqrt_(u1);
+    const float alpha = acosf_(cos_alpha);
+    const float phi = two_pi_times(u2);
+    const float r = sinf_small_(alpha);
+    float sp, cp;
+    sincosf_small_(phi, &sp, &cp);
+    return v3(r * cp, r * sp, cos_alpha);
+}
+
+// --------------------------------------------------------------- geometry
+// intersection_with_box_plane (geometric_utils.cpp:8-26) for plane = sgn*e_a.
+// dot(d, sgn*e_a) == sgn*d_a and dot(o, sgn*e_a) == sgn*o_a exactly whenever
+// the result is used (the discarded zero products only change the sign of a
+// zero, and a zero dot is rejected by the |.|<1e-6 test); d is finite.
+IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
+    const float dp = sgn * da;
+    if (lt_1em6(fabs_(dp))) return inf_();
+    const float t = (1.0f - sgn * oa) / dp;
+    const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
+    if (fabs_(px) > 1.0f || fabs_(py) > 1.0f || fabs_(pz) > 1.0f) return inf_();
+    if (dp < 0.0f) return inf_();
+    if (lt_1em6(t)) return inf_();
+    return t;
+}
+
+// intersection_with_sphere (geometric_utils.cpp:28-55). The f64 expression
+// (float)((-2.0*b -+ sqrt_desc)/2.0) equals (-2b -+ sqrt_desc)*0.5f in f32:
+// both operands are floats, so the f64 difference is exact whenever it can
+// affect the f32 rounding (see DESIGN.md "mixed precision").
+IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
+    const float b = dot(o, d);
+    const float desc = 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
+    if (desc < 0.0f) return inf_();
+    const float sd = sqrt_(desc);
+    const float m2b = -2.0f * b;
+    float t1 = (m2b - sd) * 0.5f;
+    float t2 = (m2b + sd) * 0.5f;
+    if (lt_1em6(t1)) t1 = inf_();
+    if (lt_1em6(t2)) t2 = inf_();
+    const float t = (t2 < t1) ? t2 : t1;  // std::min(t1, t2)
+    if (t == inf_()) return t;            // pos would be inf/nan; the test then keeps t
+    const vec3 pos = o + d * t;
+    if (dot(pos, o - pos) <= 0.0f) return inf_();
+    return t;
+}
+
+// GeometrySphereInBox::traceRay (GeometrySphereInBox.cpp:10-81) nearest hit:
+// returns t (inf = miss) and the hit primitive: 0..4 = plane index in the
+// reference's order {+x,+y,+z,-x,-z}, 5 = the r=0.5 sphere.
+IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
+    float best = inf_();
+    int bi = -1;
+    if (d.x + d.y + d.z != d.x + d.y + d.z) {  // NaN direction: every test fails
+        *prim = -1;
+        return best;
+    }
+    // x: the facing plane is +x (index 0) for d.x>0 and -x (index 3) otherwise
+    {
+        const float s = d.x > 0.0f ? 1.0f : -1.0f;
+        const float t = box_plane_t(o.x, d.x, s, o, d);
+        const int i = d.x > 0.0f ? 0 : 3;
+        best = t;
+        bi = i;
+    }
+    {
+        const float t = d.y > 0.0f ? box_plane_t(o.y, d.y, 1.0f, o, d) : inf_();
+        if (t < best || (t == best && 1 < bi && t != inf_())) { best = t; bi = 1; }
+    }
+    {
+        const float s = d.z > 0.0f ? 1.0f : -1.0f;
+        const float t = box_plane_t(o.z, d.z, s, o, d);
+        const int i = d.z > 0.0f ? 2 : 4;
+        if (t < best || (t == best && i < bi && t != inf_())) { best = t; bi = i; }
+    }
+    if (best == inf_()) bi = -1;
+    *prim = bi;
+    return best;
+}
+IPT_HD float trace_box(vec3 o, vec3 d, int* prim) {
+    int bi;
+    float best = trace_box_planes_only(o, d, &bi);
+    const float ts = sphere_t(0.5f, o, d);
+    if (ts < best) { best = ts; bi = 5; }
+    *prim = bi;
+    return best;
+}
+// FractalSpheres' acceptance "std::abs(dist) > 1e-6" (double literal):
+// |t| > 1e-6 <=> |t| > float(1e-6) = 0x358637bd.
+IPT_HD bool gt_1em6(float f) { return f > u2f(0x358637bdu); }
+
+// ----------------------------------------------------------------- lights
+// AreaLight::traceRay (lighting.cpp:107-144); returns hit flag, position.
+IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit) {
+    const float n_dir = dot(L.n, d);
+    if (lt_1em6(fabs_(n_dir)) || n_dir > 0.0f) return false;
+    const float t = dot(L.n, L.P - o) / n_dir;
+    if (lt_1em6(t)) return false;
+    const vec3 rel = (o + d * t) - L.P;
+    const vec3 coord = mul(L.inv, rel);
+    bool h;
+    if (L.type == 0)
+        h = coord.x >= 0.0f && coord.x <= 1.0f && coord.y >= 0.0f && coord.y <= 1.0f;
+    else
+        h = coord.x >= 0.0f && coord.y >= 0.0f && coord.x + coord.y <= 1.0f;
+    if (!h) return false;
+    *hit = L.P + rel;
+    return true;
+}
+
+// DdfFromLight::value for a direction whose light trace is `has`/`hit`
+// (lighting.cpp:136-148).
+IPT_HD float light_pdf(const LightDev& L, vec3 o, bool has, vec3 hit) {
+    if (!has) return 0.0f;
+    const vec3 dir = normalize(hit - o);
+    const float cosinus = dot(L.n, -dir);
+    if (cosinus < 0.0f) return 0.0f;
+    const vec3 ho = hit - o;
+    const float decay = dot(ho, ho);
+    return decay / cosinus / L.area;
+}
+
+// DdfFromLight::sample via AreaLight::sample (lighting.cpp:125-134, 93-104).
+// Returns vec3() when the sampled point faces away (cosinus < 1e-5f).
+IPT_HD vec3 light_sample_dir(const LightDev& L, vec3 o, float u1, float u2raw) {
+    const float u2 = u2raw * (L.type == 1 ? 1.0f - u1 : 1.0f);
+    const vec3 pos = (L.x * u1 + L.y * u2) + L.P;
+    const vec3 dir = normalize(pos - o);
+    const float cosinus = dot(L.n, -dir);
+    if (cosinus < 1e-5f) return v3(0.0f, 0.0f, 0.0f);
+    return dir;
+}
+
+// AreaLight constructor derived fields (lighting.cpp:79-90) + the per-call
+// normal/power expressions of traceRay/sample.
+IPT_HD LightDev make_light(vec3 P, vec3 x, vec3 y, float power, int type) {
+    LightDev L;
+    L.P = P;
+    L.x = x;
+    L.y = y;
+    L.type = type;
+    L.pad = 0;
+    const float full_area = length(cross(x, y));
+    L.area = type == 0 ? full_area : full_area / 2.0f;
+    mat3 m;
+    m.c[0] = x;
+    m.c[1] = y;
+    m.c[2] = cross(x, y);
+    L.inv = inverse(m);
+    L.n = normalize(cross(x, y));
+    L.spow = power / L.area;
+    return L;
+}
+
+// ------------------------------------------------------------ camera/pixel
+// render_sample jitter (main.cpp:192-198) generalised from 640 to W/H.
+IPT_HD float jitter_coord(int i, float u, int n) {
+    float x = ((float)i + u) / (float)n;
+    if (x == 1.0f) x = u2f(0x3f7fffffu);  // nextafter(1.0f, 0.0f)
+    return x;
+}
+// SimpleCamera::sampleRay (SimpleCamera.cpp:15-21)
+IPT_HD vec3 camera_dir(vec3 right, vec3 up, vec3 direction, float x, float y) {
+    x -= 0.5f;
+    y -= 0.5f;
+    const vec3 ray = right * x + up * y + direction;
+    return normalize(ray);
+}
+// GridRenderPlane::addRay index mapping (GridRenderPlane.cpp:66-67).
+IPT_HD void grid_index(float x, float y, int W, int H, int* xi, int* yi) {
+    const float fx = x * (float)W;
+    const float fy = ((float)H - y * (float)H) - 1.0f;
+    *xi = fx < 0.0f ? 0 : (int)fx;  // (size_t) truncation; values in (-1,0) -> 0
+    *yi = fy < 0.0f ? 0 : (int)fy;
+}
+IPT_HD int nominal_row(int iy, int H) { return H - 2 - iy > 0 ? H - 2 - iy : 0; }
+
+// ---------------------------------------------------------- mixture weights
+// CollectionLighting::distributionInPoint + unite (CollectionLighting.cpp:12-21,
+// ddf.cpp:169-235) followed by main.cpp:143's unite(light_ddf,1, sdf,1).
+// Point-independent: w[0..n-1] lights, w[n] the surface BRDF.
+inline void mixture_weights(const float* powers, int n, float* w) {
+    float acc_power = 0.0f;
+    int cnt = 0;
+    for (int l = 0; l < n; ++l) {
+        const float ka = acc_power, kb = powers[l];
+        if (cnt == 0 && ka != 0.0f) {
+            // unite(nullptr,0,b,kb) -> unite(Union(),0,b,1.0f) -> [b : 1/(0+1)]
+            w[0] = 1.0f / (0.0f + 1.0f);
+            cnt = 1;
+        } else {
+            for (int k = 0; k < cnt; ++k) w[k] *= ka / (ka + kb);
+            w[cnt++] = kb / (ka + kb);
+        }
+        acc_power += powers[l];
+    }
+    if (cnt == 0) {
+        w[0] = 1.0f / (0.0f + 1.0f);
+        return;
+    }
+    for (int k = 0; k < cnt; ++k) w[k] *= 1.0f / (1.0f + 1.0f);
+    w[cnt] = 1.0f / (1.0f + 1.0f);
+}
+
+}  // namespace ipt

@@ -1,0 +1,121 @@
+"""Scene descriptions for the C-ABI, built with the reference's constructor
+arithmetic (float32, glm operation order) so that the flattened values equal
+the fields of the reference objects bit-for-bit.
+
+make_scene_box()       sample_scenes[0] (reference src/sample_scenes.cpp:20-41)
+make_scene_box_lights  the [0] light split into k x k co-planar squares
+                       (BASELINE.json configs[4])
+make_scene_spheres     box planes + N seeded spheres (configs[2])
+
+The C++ mirror (ipt_amd/host/sample_scenes.cpp) builds the same scenes for
+C++ callers; tests check the two agree.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .capi import IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES_IN_BOX, IPT_LIGHT_AREA_DIAMOND
+
+f32 = np.float32
+
+
+def _v(*a):
+    return np.array(a, dtype=f32)
+
+
+def dot(a, b):
+    t = (a * b).astype(f32)
+    return f32(f32(t[0] + t[1]) + t[2])
+
+
+def cross(x, y):
+    return np.array([f32(x[1] * y[2]) - f32(y[1] * x[2]),
+                     f32(x[2] * y[0]) - f32(y[2] * x[0]),
+                     f32(x[0] * y[1]) - f32(y[0] * x[1])], dtype=f32)
+
+
+def normalize(v):
+    s = f32(f32(1.0) / np.sqrt(dot(v, v), dtype=f32))
+    return (v * s).astype(f32)
+
+
+def simple_camera(position, direction, up_hint=(0.0, 0.0, 1.0)):
+    """SimpleCamera ctor (reference src/SimpleCamera.cpp:8-13)."""
+    position = _v(*position)
+    direction = _v(*direction)
+    right = normalize(cross(direction, _v(*up_hint)))
+    up = normalize(cross(right, direction))
+    return {"position": position.tolist(), "direction": direction.tolist(),
+            "right": right.tolist(), "up": up.tolist()}
+
+
+def square_light(corner, normal, x_side, power=1.0):
+    """CollectionLighting::addSquareLight (CollectionLighting.cpp:42-46)."""
+    corner = _v(*corner)
+    x_side = _v(*x_side)
+    y_side = cross(_v(*normal), x_side)
+    return {"position": corner.tolist(), "x_axis": x_side.tolist(), "y_axis": y_side.tolist(),
+            "power": float(f32(power)), "type": IPT_LIGHT_AREA_DIAMOND}
+
+
+def box_camera():
+    # sample_scenes.cpp:36-38
+    camera_pos = _v(0.0, -3.0, 0.1)
+    camera_dir = normalize((_v(0.0, 1.0, -1.0) - camera_pos).astype(f32))
+    return simple_camera(camera_pos, camera_dir)
+
+
+def box_light_corner():
+    # vec3{+0.1f, -0.8f-0.1f, -0.15f}: -0.8f-0.1f is a float subtraction
+    return (f32(0.1), f32(f32(-0.8) - f32(0.1)), f32(-0.15))
+
+
+def make_scene_box():
+    """sample_scenes[0]: GeometrySphereInBox + one 0.2x0.2 square light."""
+    light = square_light(box_light_corner(), (0.0, 0.0, -1.0), (0.0, 0.2, 0.0), 1.0)
+    return {"geometry_kind": IPT_GEOM_SPHERE_IN_BOX, "lights": [light], "spheres": [],
+            "camera": box_camera()}
+
+
+def make_scene_box_lights(k: int = 16):
+    """The [0] light split into k*k co-planar squares of power 1/k^2 each, via
+    the public addSquareLight. Expected image equals [0]'s."""
+    c0 = box_light_corner()
+    side = f32(f32(0.2) / f32(k))
+    lights = []
+    for a in range(k):
+        for b in range(k):
+            corner = (f32(c0[0] + f32(f32(b) * side)), f32(c0[1] + f32(f32(a) * side)), c0[2])
+            lights.append(square_light(corner, (0.0, 0.0, -1.0), (0.0, float(side), 0.0),
+                                       float(f32(1.0) / f32(k * k))))
+    return {"geometry_kind": IPT_GEOM_SPHERE_IN_BOX, "lights": lights, "spheres": [],
+            "camera": box_camera()}
+
+
+def splitmix64(seed):
+    x = np.uint64(seed)
+    while True:
+        x = np.uint64(x + np.uint64(0x9E3779B97F4A7C15))
+        z = x
+        z = np.uint64((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9))
+        z = np.uint64((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB))
+        yield int(z ^ (z >> np.uint64(31)))
+
+
+def make_scene_spheres(n: int = 10000, seed: int = 1):
+    """Box planes + n random spheres (centres uniform in [-0.9,0.9]^3, radius in
+    [0.01,0.03], SplitMix64(seed)), same camera and light as [0]."""
+    g = splitmix64(seed)
+
+    def u():
+        return f32((next(g) >> 40) * (1.0 / (1 << 24)))
+
+    spheres = []
+    with np.errstate(over="ignore"):
+        for _ in range(n):
+            c = [float(f32(f32(-0.9) + f32(f32(1.8) * u()))) for _ in range(3)]
+            r = float(f32(f32(0.01) + f32(f32(0.02) * u())))
+            spheres.append((c, r))
+    light = square_light(box_light_corner(), (0.0, 0.0, -1.0), (0.0, 0.2, 0.0), 1.0)
+    return {"geometry_kind": IPT_GEOM_SPHERES_IN_BOX, "lights": [light], "spheres": spheres,
+            "camera": box_camera()}

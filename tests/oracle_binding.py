@@ -1,0 +1,95 @@
+"""Test-side binding of oracle/libipt_oracle.so (the CPU restatement checker).
+
+Test infrastructure only: loaded by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE_SO = ROOT / "oracle" / "libipt_oracle.so"
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not ORACLE_SO.exists():
+        build()
+    from ipt_amd.capi import Counters, Params, Scene  # struct layouts only
+
+    lib = C.CDLL(str(ORACLE_SO))
+    lib.ipt_oracle_render_values.argtypes = [C.POINTER(Scene), C.POINTER(Params), C.c_void_p,
+                                             C.c_void_p, C.c_int, C.POINTER(Counters)]
+    lib.ipt_oracle_accumulate.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    f3 = C.POINTER(C.c_float)
+    lib.ipt_oracle_box_plane.argtypes = [f3, f3, f3]
+    lib.ipt_oracle_box_plane.restype = C.c_float
+    lib.ipt_oracle_sphere.argtypes = [C.c_float, f3, f3]
+    lib.ipt_oracle_sphere.restype = C.c_float
+    lib.ipt_oracle_trace_box.argtypes = [f3, f3, f3]
+    lib.ipt_oracle_light_trace.argtypes = [C.c_void_p, f3, f3, f3]
+    lib.ipt_oracle_area_light.argtypes = [C.c_void_p, f3]
+    lib.ipt_oracle_area_light.restype = None
+    lib.ipt_oracle_rotate.argtypes = [f3, f3]
+    lib.ipt_oracle_rotate.restype = None
+    lib.ipt_oracle_camera.argtypes = [f3, f3, f3, f3]
+    lib.ipt_oracle_camera.restype = None
+    lib.ipt_oracle_mixture_weights.argtypes = [f3, C.c_int, f3]
+    lib.ipt_oracle_mixture_weights.restype = None
+    lib.ipt_oracle_cosine_value.argtypes = [C.c_float]
+    lib.ipt_oracle_cosine_value.restype = C.c_float
+    lib.ipt_oracle_randf.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.ipt_oracle_randf.restype = C.c_float
+    _lib = lib
+    return lib
+
+
+def fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def render_values(scene_desc: dict, p, n_threads: int = 0, with_counters: bool = False):
+    from ipt_amd.capi import Counters, make_scene
+
+    lib = load()
+    s, keep = make_scene(scene_desc)
+    n = p.spp * p.width * p.height
+    vals = np.zeros(n, np.float32)
+    codes = np.zeros(n, np.uint8)
+    cnt = Counters()
+    rc = lib.ipt_oracle_render_values(C.byref(s), C.byref(p), vals.ctypes.data, codes.ctypes.data,
+                                      n_threads, C.byref(cnt) if with_counters else None)
+    assert rc == 0, rc
+    shape = (p.spp, p.height, p.width)
+    out = (vals.reshape(shape), codes.reshape(shape))
+    return out + (cnt.as_dict(),) if with_counters else out
+
+
+def accumulate(values: np.ndarray, codes: np.ndarray, img: dict | None = None):
+    """GridRenderPlane::addRay replay; returns dict(pixels, counters, sums, pixel_max)."""
+    lib = load()
+    spp, H, W = values.shape
+    if img is None:
+        img = {k: np.zeros(H * W, dt) for k, dt in
+               (("pixels", np.float32), ("counters", np.uint32), ("sums", np.float32),
+                ("pixel_max", np.float32))}
+    v = np.ascontiguousarray(values, np.float32)
+    c = np.ascontiguousarray(codes, np.uint8)
+    rc = lib.ipt_oracle_accumulate(W, H, spp, v.ctypes.data, c.ctypes.data,
+                                   img["pixels"].ctypes.data, img["counters"].ctypes.data,
+                                   img["sums"].ctypes.data, img["pixel_max"].ctypes.data)
+    assert rc == 0, rc
+    return img

@@ -1,0 +1,84 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact. Per-sample radiance values and GridRenderPlane drift codes
+must be identical to the oracle's, and the accumulated GridRenderPlane state
+(running-mean pixels, counters, sums, per-pixel max) identical to the
+oracle's replay of GridRenderPlane::addRay (GridRenderPlane.cpp:61-75).
+The BASELINE tolerance (<=1e-3 per-pixel L-inf) is asserted as well, but the
+test requires 0.
+"""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from ipt_amd import capi, scenes
+
+pytestmark = pytest.mark.gpu
+
+L_INF_TOL = 1e-3  # BASELINE.json north_star per-channel tolerance
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def _render_both(ctx, desc, p, oracle):
+    ctx.upload_scene(desc)
+    gv, gc = ctx.render_values(p)
+    ov, oc = ob.render_values(desc, p, 0)
+    return gv, gc, ov, oc
+
+
+@pytest.mark.parametrize("n_rays,depth_max", [(16, 8), (16, 4), (4, 8), (16, 0), (1, 3), (0, 5)])
+def test_values_bit_exact_box(gpu_ctx, oracle, n_rays, depth_max):
+    desc = scenes.make_scene_box()
+    p = capi.make_params(48, 40, 3, spp_offset=7, n_rays=n_rays, depth_max=depth_max)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), (
+        f"{int((_bits(gv) != _bits(ov)).sum())} of {gv.size} samples differ; "
+        f"max |d| = {np.abs(gv - ov).max()}")
+
+
+def test_image_bit_exact_box(gpu_ctx, oracle):
+    desc = scenes.make_scene_box()
+    W, H = 64, 64
+    gpu_ctx.upload_scene(desc)
+    img = {k: np.zeros(W * H, dt) for k, dt in (("pixels", np.float32), ("counters", np.uint32),
+                                                ("sums", np.float32), ("pixel_max", np.float32))}
+    # two calls continue the same running mean (spp_offset)
+    gpu_ctx.render(capi.make_params(W, H, 3, spp_offset=0), img)
+    gpu_ctx.render(capi.make_params(W, H, 2, spp_offset=3), img)
+    ov, oc = ob.render_values(desc, capi.make_params(W, H, 5, spp_offset=0))
+    ref = ob.accumulate(ov, oc)
+    for k in ("pixels", "sums", "pixel_max"):
+        assert np.array_equal(_bits(img[k]), _bits(ref[k])), k
+    assert np.array_equal(img["counters"], ref["counters"])
+    assert np.abs(img["pixels"] - ref["pixels"]).max() <= L_INF_TOL
+
+
+def test_counters_match_oracle(gpu_ctx, oracle):
+    desc = scenes.make_scene_box()
+    p = capi.make_params(32, 32, 2, flags=capi.IPT_FLAG_COUNTERS)
+    gpu_ctx.upload_scene(desc)
+    gpu_ctx.reset_counters()
+    gpu_ctx.render_values(p)
+    g = gpu_ctx.counters()
+    _, _, o = ob.render_values(desc, capi.make_params(32, 32, 2), 0, with_counters=True)
+    for k in ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
+              "iterations", "light_samples", "skipped", "light_traces", "drifted"):
+        assert g[k] == o[k], (k, g[k], o[k])
+
+
+@pytest.mark.parametrize("fn", sorted(capi.MATH_FNS.values()))
+def test_device_math_matches_host(gpu_ctx, fn):
+    """Device build of ipt_math.h == host build (which equals glibc, see
+    test_math_exhaustive.py): all 2^24 RNG-reachable inputs + a strided sweep."""
+    u = (np.arange(1 << 24, dtype=np.float32) * np.float32(2.0 ** -24))
+    sweep = np.arange(0, 0x42f00000, 997, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    neg = -sweep[::7]
+    for x in (u, np.sqrt(u, dtype=np.float32), sweep, neg):
+        d = gpu_ctx.math_device(fn, x)
+        h = capi.math_host(fn, x)
+        same = (_bits(d) == _bits(h)) | (np.isnan(d) & np.isnan(h))
+        assert same.all(), (fn, x[~same][:4], d[~same][:4], h[~same][:4])
