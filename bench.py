@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X path-tracing inner loop (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): sample_scenes[0] (make_scene_box), 1024^2,
+256 spp, n_rays 16, depth_max 8, fp32, synthetic = the scene itself.
+A *step* renders `--spp-per-step` sample passes of the whole frame (one
+ipt_render_device call: path kernel + GridRenderPlane accumulate kernel); the
+default 8 steps x 32 spp is the full 256-spp frame.
+
+Multi-GPU (torchrun, one rank per GPU): the frame's destination rows are cut
+into 16-row tiles dealt round-robin to the ranks (weak scaling: the frame is
+1024 x 1024*N so each rank keeps the 1-GPU workload); the path needs no
+data-path collective, and the finished frame is assembled on rank 0 by one
+RCCL reduce per GridRenderPlane buffer at the end of the timed region.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp-per-step", type=int, default=32)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=1024, help="per-rank share of frame rows")
+    ap.add_argument("--n-rays", type=int, default=16)
+    ap.add_argument("--depth-max", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=20241223)
+    ap.add_argument("--tile-rows", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target duration of the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-counters", action="store_true",
+                    help="skip the (untimed) counting re-render used for the roofline")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, desc):
+    """Oracle restatement timed on host cores over a strided row sample."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import ctypes as C
+
+    import oracle_binding
+    from ipt_amd import capi
+
+    lib = oracle_binding.load()
+    lib.ipt_oracle_render_rows.argtypes = [C.POINTER(capi.Scene), C.POINTER(capi.Params), C.c_int,
+                                           C.c_int, C.c_int, C.POINTER(C.c_uint64)]
+    lib.ipt_oracle_render_rows.restype = C.c_double
+    s, keep = capi.make_scene(desc)
+    W = args.width
+    H = args.height
+    threads = args.cpu_threads
+    row_step = 64  # 16 rows of the 1024-row frame per phase
+    total_paths = 0
+    t0 = time.perf_counter()
+    phase = 0
+    while True:
+        p = capi.make_params(W, H, 1, spp_offset=phase // row_step, n_rays=args.n_rays,
+                             depth_max=args.depth_max, seed=args.seed)
+        n = C.c_uint64()
+        lib.ipt_oracle_render_rows(C.byref(s), C.byref(p), row_step, phase % row_step, threads,
+                                   C.byref(n))
+        total_paths += n.value
+        phase += 37  # co-prime stride over row phases: an unbiased row sample
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    rows = (phase // 37)
+    return {
+        "value": total_paths / el / 1e6,
+        "unit": "Mpaths/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{rows} x 16 source rows of the {W}x{H} frame (1 pass each, rows strided "
+                   f"by 64 at phases 37k mod 64), {total_paths} paths in {el:.1f} s, "
+                   f"{threads} threads; oracle/ipt_oracle.cpp (recursive CPU restatement, "
+                   f"glibc libm)"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from ipt_amd import capi, roofline, scenes
+
+    desc = scenes.make_scene_box()
+    ctx = capi.Context(local_rank)
+    ctx.upload_scene(desc)
+
+    W = args.width
+    H = args.height * world  # weak scaling: the frame grows with the rank count
+    npix = W * H
+    pixels = torch.zeros(npix, dtype=torch.float32, device=dev)
+    counters = torch.zeros(npix, dtype=torch.int32, device=dev)
+    sums = torch.zeros(npix, dtype=torch.float32, device=dev)
+    pmax = torch.zeros(npix, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def params(spp, off, flags=0):
+        return capi.make_params(W, H, spp, spp_offset=off, n_rays=args.n_rays,
+                                depth_max=args.depth_max, seed=args.seed,
+                                tile_rows=args.tile_rows if world > 1 else 0, n_shards=world,
+                                shard_id=rank, flags=flags)
+
+    def render(p):
+        ctx.render_device(p, pixels.data_ptr(), counters.data_ptr(), sums.data_ptr(),
+                          pmax.data_ptr(), stream)
+
+    # warmup (separate passes, then reset the image)
+    for i in range(args.warmup):
+        render(params(args.spp_per_step, 1_000_000 + i * args.spp_per_step))
+    for t in (pixels, counters, sums, pmax):
+        t.zero_()
+    torch.cuda.synchronize(dev)
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    path_ms = acc_ms = 0.0
+    for step in range(args.steps):
+        render(params(args.spp_per_step, step * args.spp_per_step))
+        pm, am = ctx.last_kernel_ms()
+        path_ms += pm
+        acc_ms += am
+    if dist:
+        # frame end: assemble the GridRenderPlane on rank 0 (each pixel is owned
+        # by exactly one rank, the others hold zeros)
+        dist.reduce(pixels, 0, op=dist.ReduceOp.SUM)
+        dist.reduce(counters, 0, op=dist.ReduceOp.SUM)
+        dist.reduce(sums, 0, op=dist.ReduceOp.SUM)
+        dist.reduce(pmax, 0, op=dist.ReduceOp.MAX)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed, path_ms, acc_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, path_ms, acc_ms = tt.tolist()
+
+    spp_total = args.steps * args.spp_per_step
+    total_paths = W * H * spp_total
+    value = total_paths / elapsed / 1e6
+
+    # algorithmic op count of the timed work: re-render the same passes with
+    # the kernel's event counters (untimed; counts are deterministic)
+    roof = None
+    cnt = None
+    if not args.no_counters:
+        sv = [t.clone() for t in (pixels, counters, sums, pmax)]
+        ctx.reset_counters()
+        for step in range(args.steps):
+            render(params(args.spp_per_step, step * args.spp_per_step, capi.IPT_FLAG_COUNTERS))
+        torch.cuda.synchronize(dev)
+        cnt = ctx.counters()
+        for t, s in zip((pixels, counters, sums, pmax), sv):
+            t.copy_(s)
+        if dist:
+            ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64, device=dev)
+            dist.all_reduce(ct)
+            cnt = dict(zip(capi.COUNTER_NAMES, [int(x) for x in ct.tolist()]))
+        ops = roofline.ops_from_counters(cnt)
+        # per launch on one rank: ops/world per launch, average launch duration
+        launch_s = path_ms / 1e3 / args.steps
+        achieved = ops / world / args.steps / launch_s
+        own_pix = npix // world
+        acc_bytes = roofline.accumulate_bytes(own_pix, args.spp_per_step)
+        acc_launch_s = acc_ms / 1e3 / args.steps
+        roof = {
+            "bound": "valu",
+            "achieved": achieved / 1e12,
+            "peak": roofline.VALU_PEAK_LANE_OPS / 1e12,
+            "unit": "Tlane-op/s",
+            "frac": achieved / roofline.VALU_PEAK_LANE_OPS,
+            "traffic": None,
+            "kernel": "path_kernel",
+            "ops_per_path": ops / cnt["paths"],
+            "launch_ms": launch_s * 1e3,
+            "note": ("algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
+                     "counters) per launch / HIP-event launch time; VALU issue peak "
+                     "256CU x 4 SIMD32 x 2.4GHz; path kernel compulsory HBM is 5 B/path"),
+            "hbm": {
+                "kernel": "accumulate_kernel",
+                "bound": "hbm",
+                "achieved": acc_bytes / acc_launch_s / 1e9 if acc_launch_s > 0 else None,
+                "peak": roofline.HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": (acc_bytes / acc_launch_s / 1e9 / roofline.HBM_PEAK_GBPS
+                         if acc_launch_s > 0 else None),
+                "launch_ms": acc_launch_s * 1e3,
+                "path_kernel_algorithmic_GBps": roofline.path_bytes(total_paths // world // args.steps) / launch_s / 1e9,
+            },
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        try:
+            cpu = cpu_baseline(args, desc)
+        except Exception as e:  # the GPU number stands on its own
+            cpu = {"error": repr(e)}
+
+    if rank == 0:
+        out = {
+            "metric": "Mpaths/sec at 1024^2, 8-bounce, sample_scenes[0]; achieved HBM GB/s",
+            "value": value,
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (sample_scenes[0] geometry/light/camera, Philox per-path RNG)",
+            "config": {"workload": f"sample_scenes[0] {W}x{H}, {spp_total} spp, depth_max "
+                                   f"{args.depth_max}, n_rays {args.n_rays}",
+                       "width": W, "height": H, "spp": spp_total,
+                       "spp_per_step": args.spp_per_step, "depth_max": args.depth_max,
+                       "n_rays": args.n_rays, "tile_rows": args.tile_rows if world > 1 else 0,
+                       "parallelism": f"tiles{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
+            "events_per_path": ({k: cnt[k] / cnt["paths"] for k in cnt if k != "paths"}
+                                if cnt else None),
+            "mean_pixel": float(pixels.mean().item()),
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,65 @@
+"""Algorithmic cost model of the hot path and gfx950 peaks.
+
+The path kernel is FP32-VALU / divergence bound (no MFMA, compulsory HBM
+traffic ~5 B per path), so its roofline is the VALU issue rate. The op count
+is ALGORITHMIC: the reference's own arithmetic per event, counted as written
+(no credit for work the GPU kernel avoids, e.g. precomputed wall frames), with
+each transcendental (acos, sin, cos) at 20 op-eq. Event counts come from the
+kernel's own counters (ipt_counters), which tests pin equal to the oracle's.
+"""
+from __future__ import annotations
+
+# gfx950 (MI355X): 256 CU x 4 SIMD-32, wave64 VALU instruction every 2 cycles
+# per SIMD at 2.4 GHz -> 256*4*32*2.4e9 = 78.6e12 lane-ops/s (the 157.3 TFLOP/s
+# FP32 spec counts an FMA as 2; the reference's arithmetic has no FMAs and must
+# not be contracted). /opt/skills/guides/MI355X_MICROARCH.md "Chip-level".
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+HBM_PEAK_GBPS = 8000.0  # spec; ~6.3 TB/s achievable (guide §HBM)
+TRANSC_OP_EQ = 20
+
+# per-event FP op counts
+OPS = {
+    "camera": 28,            # camera + jitter, per path
+    "geom_trace": 130,       # box: 127 miss / 133 hit
+    "light_trace": 57,       # area light trace (miss cost; hits +23 are in light_hit)
+    "occlusion": 18,         # light-vs-geometry length compare, per light hit
+    "rotate_build": 109,     # RotateDdf built by every geometry hit (GeometrySphereInBox.cpp:63-74)
+    "mixture_weights": 8,    # unite() weights, per expanded node
+    "sphere_normal": 10,     # per sphere-hit frame
+    "iter_light_kept": 207,  # light-sampled branch iteration, kept
+    "iter_cosine": 118,      # cosine-sampled branch iteration
+    "iter_skipped": 56,      # skipped (back-facing light sample)
+    "node_finalize": 1,
+}
+TRANSC = {"rotate_build": 3, "iter_cosine": 4}
+
+
+def ops_from_counters(c: dict) -> float:
+    """Algorithmic op-eq for a set of ipt_counters (box-family scenes)."""
+    kept_light = c["light_samples"] - c["skipped"]
+    cosine = c["iterations"] - c["light_samples"]
+    f = (c["paths"] * OPS["camera"]
+         + c["traced_rays"] * (OPS["geom_trace"] + OPS["light_trace"])
+         + c["light_hits"] * OPS["occlusion"]
+         + c["surface_hits"] * (OPS["rotate_build"] + TRANSC["rotate_build"] * TRANSC_OP_EQ)
+         + c["expanded_nodes"] * OPS["mixture_weights"]
+         + c["sphere_frames"] * OPS["sphere_normal"]
+         + kept_light * OPS["iter_light_kept"]
+         + cosine * (OPS["iter_cosine"] + TRANSC["iter_cosine"] * TRANSC_OP_EQ)
+         + c["skipped"] * OPS["iter_skipped"]
+         + c["expanded_nodes"] * OPS["node_finalize"])
+    return float(f)
+
+
+def accumulate_bytes(n_dest_pixels: int, spp: int, with_sums: bool = True,
+                     with_max: bool = True) -> int:
+    """Algorithmic HBM bytes of one accumulate launch: the radiance buffer read
+    once (4 B per sample) + the GridRenderPlane state read and written."""
+    state = 8 + (4 if with_sums else 0) + (4 if with_max else 0)
+    return n_dest_pixels * (4 * spp + 2 * state)
+
+
+def path_bytes(paths: int) -> int:
+    """Algorithmic HBM bytes of one path launch: 4 B radiance + 1 B drift code
+    written per path (scene data is a few hundred bytes, read once per CU)."""
+    return 5 * paths

@@ -681,3 +681,43 @@ float ipt_oracle_randf(uint64_t seed, uint32_t pass, uint32_t pixel, uint32_t k)
     return v;
 }
 }
+
+extern "C" {
+// CPU-baseline leg of bench.py: renders source rows iy = row_phase (mod
+// row_step) of every pass in p with n_threads threads and returns the sum of
+// the clamped values (so nothing is optimised away); *paths = samples done.
+double ipt_oracle_render_rows(const ipt_scene* scene, const ipt_params* p, int row_step,
+                              int row_phase, int n_threads, uint64_t* paths) {
+    SceneO sc = make_scene(scene);
+    Mixture mix = build_mixture(sc);
+    Ctx cx{&sc, &mix, p->depth_max};
+    const int W = p->width, H = p->height;
+    std::vector<int> rows;
+    for (int iy = row_phase; iy < H; iy += row_step) rows.push_back(iy);
+    const int64_t nrows = (int64_t)p->spp * (int64_t)rows.size();
+    std::atomic<int64_t> next{0};
+    if (n_threads <= 0) n_threads = (int)std::thread::hardware_concurrency();
+    std::vector<double> part(n_threads, 0.0);
+    auto work = [&](int tid) {
+        double acc = 0.0;
+        for (;;) {
+            int64_t r = next.fetch_add(1);
+            if (r >= nrows) break;
+            int s = (int)(r / (int64_t)rows.size());
+            int iy = rows[r % (int64_t)rows.size()];
+            for (int ix = 0; ix < W; ++ix) {
+                int xi, yi;
+                acc += oracle_pixel(cx, p, ix, iy, s, &xi, &yi);
+            }
+        }
+        part[tid] = acc;
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(work, t);
+    for (auto& t : th) t.join();
+    double total = 0.0;
+    for (double v : part) total += v;
+    if (paths) *paths = (uint64_t)nrows * (uint64_t)W;
+    return total;
+}
+}
