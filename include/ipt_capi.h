@@ -123,9 +123,9 @@ typedef struct ipt_image {
 typedef struct ipt_counters {
     uint64_t paths;           /* root ray_power calls */
     uint64_t traced_rays;     /* Geometry::traceRay calls */
-    uint64_t surface_hits;    /* rays whose nearest visible hit is geometry */
-    uint64_t light_hits;      /* rays returning a light's power */
-    uint64_t expanded_nodes;  /* nodes that ran the branch loop (n_rays > 0) */
+    uint64_t surface_hits;    /* Geometry::traceRay calls that hit */
+    uint64_t light_hits;      /* Lighting::traceRayToLight calls that hit */
+    uint64_t expanded_nodes;  /* distributionInPoint calls (surface nodes) */
     uint64_t iterations;      /* UnionDdf::sample calls */
     uint64_t light_samples;   /* iterations that sampled a light component */
     uint64_t skipped;         /* iterations that returned vec3() */
@@ -158,6 +158,12 @@ int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, voi
    (bits 0-1: dx+1, bits 2-3: dy+1 relative to the nominal destination
    (ix, max(H-2-iy,0)); 0x05 = nominal). Host buffers of spp*width*height. */
 int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t* codes);
+
+/* Host-only (no device needed): the tile plan of a sharded render.
+   owned_rows[H] = 1 for destination rows this shard accumulates;
+   cand_rows[*n_cand] = source rows whose samples it traces (the nominal
+   sources of its rows +-1 for GridRenderPlane drift). Arrays sized H. */
+int ipt_shard_plan(const ipt_params* p, uint8_t* owned_rows, int32_t* cand_rows, int32_t* n_cand);
 
 int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out);
 int ipt_reset_counters(ipt_ctx* ctx);

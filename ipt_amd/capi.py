@@ -79,6 +79,7 @@ EXPORTED_SYMBOLS = (
     "ipt_abi_version", "ipt_last_error", "ipt_create", "ipt_destroy", "ipt_upload_scene",
     "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
+    "ipt_shard_plan",
 )
 
 _lib = None
@@ -114,6 +115,7 @@ def load(path: str | os.PathLike | None = None):
     lib.ipt_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
     lib.ipt_math_host.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
     lib.ipt_math_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
+    lib.ipt_shard_plan.argtypes = [C.POINTER(Params), C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)]
     if path is None:
         _lib = lib
     return lib
@@ -247,3 +249,15 @@ def math_host(fn: int, x: np.ndarray) -> np.ndarray:
 
 MATH_FNS = {"acosf": 0, "sinf": 1, "cosf": 2, "acos_f64_f32": 3, "sincosf_sin": 4,
             "sincosf_cos": 5, "sqrtf": 6, "div_pi": 7, "two_pi_times": 8}
+
+
+def shard_plan(p: Params):
+    """(owned_rows bool[H], candidate source rows int[]) of a sharded render."""
+    lib = load()
+    owned = np.zeros(p.height, np.uint8)
+    cand = np.zeros(p.height, np.int32)
+    n = C.c_int32()
+    rc = lib.ipt_shard_plan(C.byref(p), owned.ctypes.data, cand.ctypes.data, C.byref(n))
+    if rc != IPT_OK:
+        raise IptError(rc, "ipt_shard_plan")
+    return owned.astype(bool), cand[:n.value].copy()

@@ -928,6 +928,16 @@ int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t*
     return IPT_OK;
 }
 
+int ipt_shard_plan(const ipt_params* p, uint8_t* owned_rows, int32_t* cand_rows, int32_t* n_cand) {
+    if (!p || !owned_rows || !cand_rows || !n_cand || p->height <= 0) return IPT_E_INVALID;
+    std::vector<int> rows, of_row;
+    candidate_rows(p, rows, of_row);
+    for (int y = 0; y < p->height; ++y) owned_rows[y] = owned_host(p, y) ? 1 : 0;
+    for (size_t i = 0; i < rows.size(); ++i) cand_rows[i] = rows[i];
+    *n_cand = (int32_t)rows.size();
+    return IPT_OK;
+}
+
 int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
     if (!ctx || !out) return IPT_E_INVALID;
     hipSetDevice(ctx->device);

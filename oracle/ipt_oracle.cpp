@@ -721,3 +721,84 @@ double ipt_oracle_render_rows(const ipt_scene* scene, const ipt_params* p, int r
     return total;
 }
 }
+
+extern "C" {
+// AreaLight::sample with explicit draws (lighting.cpp:93-104): pos(3), normal(3)
+void ipt_oracle_light_sample_uv(const ipt_area_light* L, float u1, float u2raw, float* out6) {
+    AreaLightO l(mk(L->position[0], L->position[1], L->position[2]),
+                 mk(L->x_axis[0], L->x_axis[1], L->x_axis[2]),
+                 mk(L->y_axis[0], L->y_axis[1], L->y_axis[2]), L->power, L->type);
+    float u2 = u2raw * (l.type == 1 ? 1.0f - u1 : 1.0f);
+    V3 pos = l.x_axis * u1 + l.y_axis * u2;
+    V3 p = pos + l.position;
+    V3 n = normalize(cross(l.x_axis, l.y_axis));
+    out6[0] = p.x; out6[1] = p.y; out6[2] = p.z;
+    out6[3] = n.x; out6[4] = n.y; out6[5] = n.z;
+}
+// SimpleCamera::sampleRay (SimpleCamera.cpp:15-21): direction(3)
+void ipt_oracle_camera_ray(const float* dir, const float* right, const float* up, float x,
+                           float y, float* out3) {
+    x -= 0.5f;
+    y -= 0.5f;
+    V3 ray = mk(right[0], right[1], right[2]) * x + mk(up[0], up[1], up[2]) * y +
+             mk(dir[0], dir[1], dir[2]);
+    V3 d = normalize(ray);
+    out3[0] = d.x; out3[1] = d.y; out3[2] = d.z;
+}
+// CollectionLighting::traceRayToLight over n lights: returns hit, pos(3), power
+int ipt_oracle_collection_trace(const ipt_area_light* L, int n, const float* o, const float* d,
+                                float* out4) {
+    SceneO sc;
+    for (int i = 0; i < n; ++i)
+        sc.lights.emplace_back(mk(L[i].position[0], L[i].position[1], L[i].position[2]),
+                               mk(L[i].x_axis[0], L[i].x_axis[1], L[i].x_axis[2]),
+                               mk(L[i].y_axis[0], L[i].y_axis[1], L[i].y_axis[2]), L[i].power,
+                               L[i].type);
+    V3 p;
+    float s;
+    if (!lighting_trace(sc, mk(o[0], o[1], o[2]), mk(d[0], d[1], d[2]), &p, &s)) return 0;
+    out4[0] = p.x; out4[1] = p.y; out4[2] = p.z; out4[3] = s;
+    return 1;
+}
+// GridRenderPlane::addRay on an explicit (x, y, v) sequence (GridRenderPlane.cpp:61-75)
+void ipt_oracle_grid_addray(int W, int H, int n, const float* xyv, float* pixels,
+                            uint32_t* counters, float* max_value) {
+    float mx = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        float x = xyv[3 * i], y = xyv[3 * i + 1], v = xyv[3 * i + 2];
+        size_t xi = x * (size_t)W;
+        float fy = (size_t)H - y * (size_t)H - 1;
+        size_t yi = fy;
+        size_t d = yi * W + xi;
+        size_t c = counters[d];
+        pixels[d] = (pixels[d] * c + v) / (c + 1);
+        counters[d] = (uint32_t)(c + 1);
+        if (pixels[d] > mx) mx = pixels[d];
+    }
+    *max_value = mx;
+}
+}
+
+extern "C" {
+// n samples of RotateDdf(CosineDdf, to)::sample (ddf_detail.h:69-72, ddf.cpp:223-231)
+// drawn from the per-path stream (seed, pass 0, pixel 0); for the chi^2 test.
+void ipt_oracle_cosine_samples(uint64_t seed, const float* to, int n, float* out3n) {
+    Rng rng;
+    rng.k0 = (uint32_t)seed;
+    rng.k1 = (uint32_t)(seed >> 32);
+    rng.s = 0;
+    rng.p = 0;
+    g_rng = &rng;
+    RotatedCosine r(mk(to[0], to[1], to[2]));
+    for (int i = 0; i < n; ++i) {
+        V3 v = r.sample();
+        out3n[3 * i] = v.x; out3n[3 * i + 1] = v.y; out3n[3 * i + 2] = v.z;
+    }
+    g_rng = nullptr;
+}
+// RotateDdf(CosineDdf, to)::value (ddf_detail.h:74-76)
+float ipt_oracle_cosine_ddf_value(const float* to, const float* d) {
+    RotatedCosine r(mk(to[0], to[1], to[2]));
+    return r.value(mk(d[0], d[1], d[2]));
+}
+}

@@ -93,3 +93,34 @@ def accumulate(values: np.ndarray, codes: np.ndarray, img: dict | None = None):
                                    img["sums"].ctypes.data, img["pixel_max"].ctypes.data)
     assert rc == 0, rc
     return img
+
+
+def setup_probes():
+    """argtypes for the KAT probes added for the reference-pinning tests."""
+    lib = load()
+    f3 = C.POINTER(C.c_float)
+    lib.ipt_oracle_light_sample_uv.argtypes = [C.c_void_p, C.c_float, C.c_float, f3]
+    lib.ipt_oracle_light_sample_uv.restype = None
+    lib.ipt_oracle_camera_ray.argtypes = [f3, f3, f3, C.c_float, C.c_float, f3]
+    lib.ipt_oracle_camera_ray.restype = None
+    lib.ipt_oracle_collection_trace.argtypes = [C.c_void_p, C.c_int, f3, f3, f3]
+    lib.ipt_oracle_grid_addray.argtypes = [C.c_int, C.c_int, C.c_int, f3, f3,
+                                           C.POINTER(C.c_uint32), f3]
+    lib.ipt_oracle_grid_addray.restype = None
+    lib.ipt_oracle_cosine_samples.argtypes = [C.c_uint64, f3, C.c_int, f3]
+    lib.ipt_oracle_cosine_samples.restype = None
+    lib.ipt_oracle_cosine_ddf_value.argtypes = [f3, f3]
+    lib.ipt_oracle_cosine_ddf_value.restype = C.c_float
+    return lib
+
+
+def area_light_struct(P, x, y, power, typ):
+    from ipt_amd.capi import AreaLight
+
+    a = AreaLight()
+    a.position[:] = [float(v) for v in P]
+    a.x_axis[:] = [float(v) for v in x]
+    a.y_axis[:] = [float(v) for v in y]
+    a.power = float(power)
+    a.type = int(typ)
+    return a

@@ -1,0 +1,62 @@
+"""The C-ABI library loads and exports every symbol include/ipt_capi.h
+declares; without a GPU it refuses to render (no CPU fallback)."""
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from ipt_amd import capi
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared_symbols():
+    txt = (ROOT / "include" / "ipt_capi.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int|void)\s+(ipt_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_expected():
+    assert set(declared_symbols()) == set(capi.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", str(capi.LIB_PATH)], check=True,
+                         capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    lib = capi.load()
+    for s in declared_symbols():
+        assert hasattr(lib, s)
+    assert lib.ipt_abi_version() == 1
+
+
+def test_no_cpu_fallback():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(capi.IptError) as e:
+        capi.Context(0)
+    assert e.value.code == capi.IPT_E_DEVICE
+
+
+def test_shard_plan_partitions_rows():
+    H = 100
+    owners = np.zeros(H, int)
+    for n_shards in (1, 2, 3, 8):
+        owners[:] = 0
+        for s in range(n_shards):
+            p = capi.make_params(64, H, 1, tile_rows=16 if n_shards > 1 else 0,
+                                 n_shards=n_shards, shard_id=s)
+            owned, cand = capi.shard_plan(p)
+            owners += owned
+            # every source whose nominal (+-1) destination is owned is a candidate
+            for iy in range(H):
+                yn = max(H - 2 - iy, 0)
+                if any(0 <= y < H and owned[y] for y in (yn - 1, yn, yn + 1)):
+                    assert iy in cand
+            assert list(cand) == sorted(cand)
+        assert (owners == 1).all(), n_shards

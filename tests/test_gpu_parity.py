@@ -82,3 +82,32 @@ def test_device_math_matches_host(gpu_ctx, fn):
         h = capi.math_host(fn, x)
         same = (_bits(d) == _bits(h)) | (np.isnan(d) & np.isnan(h))
         assert same.all(), (fn, x[~same][:4], d[~same][:4], h[~same][:4])
+
+
+@pytest.mark.parametrize("n_shards", [2, 3])
+def test_sharded_render_matches_whole_frame(gpu_ctx, oracle, n_shards):
+    """Tile-sharded rendering (one shard per call, as one rank per GPU does)
+    assembled by summation equals the whole-frame render bit-for-bit."""
+    desc = scenes.make_scene_box()
+    W, H, tile = 40, 50, 8
+    gpu_ctx.upload_scene(desc)
+
+    def blank():
+        return {k: np.zeros(W * H, dt) for k, dt in (("pixels", np.float32), ("counters", np.uint32),
+                                                     ("sums", np.float32), ("pixel_max", np.float32))}
+
+    whole = blank()
+    gpu_ctx.render(capi.make_params(W, H, 3), whole)
+    acc = blank()
+    for s in range(n_shards):
+        part = blank()
+        p = capi.make_params(W, H, 3, tile_rows=tile, n_shards=n_shards, shard_id=s)
+        gpu_ctx.render(p, part)
+        owned, _ = capi.shard_plan(p)
+        mask = np.repeat(owned, W)
+        for k in acc:
+            assert not part[k][~mask].any(), "shard wrote outside its rows"
+            acc[k] = acc[k] + part[k]
+    for k in ("pixels", "sums", "pixel_max"):
+        assert np.array_equal(_bits(acc[k]), _bits(whole[k])), k
+    assert np.array_equal(acc["counters"], whole["counters"])
