@@ -199,13 +199,29 @@ def main():
         own_pix = npix // world
         acc_bytes = roofline.accumulate_bytes(own_pix, args.spp_per_step)
         acc_launch_s = acc_ms / 1e3 / args.steps
+        traffic = None
+        traffic_src = None
+        pmc_file = ROOT / "profiles" / "pmc_latest.json"
+        if pmc_file.exists():
+            try:
+                pm = json.load(open(pmc_file))
+                c0 = pm.get("config", {})
+                if (c0.get("width") == W and c0.get("height") == args.height
+                        and c0.get("spp_per_step") == args.spp_per_step
+                        and "path_kernel_hbm_bytes_per_launch" in pm):
+                    traffic = pm["path_kernel_hbm_bytes_per_launch"]
+                    traffic_src = f"profiles/{pm['tag']}_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, same config)"
+            except Exception:
+                traffic = None
         roof = {
             "bound": "valu",
             "achieved": achieved / 1e12,
             "peak": roofline.VALU_PEAK_LANE_OPS / 1e12,
             "unit": "Tlane-op/s",
             "frac": achieved / roofline.VALU_PEAK_LANE_OPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src,
             "kernel": "path_kernel",
             "ops_per_path": ops / cnt["paths"],
             "launch_ms": launch_s * 1e3,
