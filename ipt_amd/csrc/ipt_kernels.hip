@@ -42,20 +42,20 @@ struct KParams {
     int W, H, spp, spp_offset, n_rays, depth_max;
     uint32_t key0, key1;
     int n_cand;              // candidate source rows
-    const int* cand_rows;    // [n_cand] source row index
+    const int* __restrict__ cand_rows;    // [n_cand] source row index
     int tile_rows, n_shards, shard_id;
     unsigned long long total_units;
     unsigned long long* unit_counter;
-    float* values;           // [spp][n_cand][W]
-    uint8_t* codes;          // [spp][n_cand][W]
-    uint8_t* flags;          // [H][W]
+    float* __restrict__ values;           // [spp][n_cand][W]
+    uint8_t* __restrict__ codes;          // [spp][n_cand][W]
+    uint8_t* __restrict__ flags;          // [H][W]
     unsigned long long* counters;
     int geometry_kind;
     int n_lights;
-    const LightDev* lights;  // [n_lights]
-    const float* weights;    // [n_lights+1]
-    const float* cdf;        // [n_lights+1] sequential prefix sums of weights
-    const Frame* wall_frames;  // [5]
+    const LightDev* __restrict__ lights;  // [n_lights]
+    const float* __restrict__ weights;    // [n_lights+1]
+    const float* __restrict__ cdf;        // [n_lights+1] sequential prefix sums of weights
+    const Frame* __restrict__ wall_frames;  // [5]
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int n_spheres;
     const float4* spheres;   // (c.xyz, r)
@@ -111,14 +111,86 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
     return best;
 }
 
-template <int MAXSUSP, bool COUNT>
-__global__ __launch_bounds__(kBlock, 2) void path_kernel(KParams kp) {
+// Scene data staged once per workgroup (never re-read from HBM/L2 inside the
+// step loop): wall frames, lights (<= kLdsLights), mixture weights + CDF and
+// the candidate-row table live in LDS after the DFS stack.
+constexpr int kLdsLights = 16;
+constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
+constexpr int kLdsCand = 1024;
+__host__ __device__ constexpr size_t scene_lds_words() {
+    return 60 + (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) + kLdsCand;
+}
+
+// Where the lights live during the step loop (compile time, so that no
+// generic/flat pointer is ever formed: a flat load would make the compiler
+// wait for every outstanding radiance store).
+enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3 };
+
+template <int LMODE>
+struct LightSet {
+    const LightDev* lds;
+    const LightDev* __restrict__ glob;
+    const float* wl;  // weights in LDS
+    const float* cl;  // cdf in LDS
+    const float* __restrict__ wg;
+    const float* __restrict__ cg;
+    LightDev one;
+    float w0, c0, c1;
+    __device__ __forceinline__ const LightDev& light(int i) const {
+        if (LMODE == kLightsOne) return one;
+        if (LMODE == kLightsLds) return lds[i];
+        return glob[i];
+    }
+    __device__ __forceinline__ float weight(int i) const {
+        if (LMODE == kLightsOne) return w0;
+        if (LMODE == kLightsLds) return wl[i];
+        return wg[i];
+    }
+    __device__ __forceinline__ float cdf(int i) const {
+        if (LMODE == kLightsOne) return i == 0 ? c0 : c1;
+        if (LMODE == kLightsLds) return cl[i];
+        return cg[i];
+    }
+};
+
+template <int MAXSUSP, bool COUNT, int LMODE>
+__global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
     float* wallf = lds + MAXSUSP * kStackFields * kBlock;     // [5][12]
+    LightDev* lights_lds = reinterpret_cast<LightDev*>(wallf + 60);
+    float* weights_lds = wallf + 60 + kLdsLights * kLightWords;
+    float* cdf_lds = weights_lds + (kLdsLights + 1);
+    int* cand_lds = reinterpret_cast<int*>(cdf_lds + (kLdsLights + 1));
     const int tid = threadIdx.x;
+    const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
+    const bool cand_in_lds = sharded && kp.n_cand <= kLdsCand;
     if (tid < 60) wallf[tid] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
+    if (LMODE == kLightsLds) {
+        const float* src = reinterpret_cast<const float*>(kp.lights);
+        float* dst = reinterpret_cast<float*>(lights_lds);
+        for (int i = tid; i < kp.n_lights * kLightWords; i += kBlock) dst[i] = src[i];
+        for (int i = tid; i <= kp.n_lights; i += kBlock) {
+            weights_lds[i] = kp.weights[i];
+            cdf_lds[i] = kp.cdf[i];
+        }
+    }
+    if (cand_in_lds)
+        for (int i = tid; i < kp.n_cand; i += kBlock) cand_lds[i] = kp.cand_rows[i];
     __syncthreads();
+    LightSet<LMODE> LS;
+    LS.lds = lights_lds;
+    LS.glob = kp.lights;
+    LS.wl = weights_lds;
+    LS.cl = cdf_lds;
+    LS.wg = kp.weights;
+    LS.cg = kp.cdf;
+    if (LMODE == kLightsOne) {
+        LS.one = kp.lights[0];
+        LS.w0 = kp.weights[0];
+        LS.c0 = kp.cdf[0];
+        LS.c1 = kp.cdf[1];
+    }
 
     const int lane = tid & 63;
     const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -190,7 +262,13 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(KParams kp) {
             const unsigned long long rem = unit - s * per_pass;
             const int cand = (int)(rem / (unsigned long long)kp.W);
             const int ix = (int)(rem - (unsigned long long)cand * kp.W);
-            const int iy = kp.cand_rows[cand];
+            int iy = cand;
+            if (sharded) {
+                if (cand_in_lds)
+                    iy = cand_lds[cand];
+                else
+                    iy = kp.cand_rows[cand];
+            }
             rpass = (uint32_t)(kp.spp_offset + (int)s);
             rpix = (uint32_t)(iy * kp.W + ix);
             philox_fill(w.a0, w.a1, w.a2, w.a3, 0u, rpass, rpix, kp.key0, kp.key1);
@@ -262,14 +340,18 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(KParams kp) {
                 const float r = u01(win_at(w, j));
                 // UnionDdf::sample pick (ddf.cpp:142-153): first c with r < cdf[c]
                 int c = 0;
-                while (c <= nl && !(r < kp.cdf[c])) ++c;
+                if (LMODE == kLightsOne) {
+                    c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+                } else {
+                    while (c <= nl && !(r < LS.cdf(c))) ++c;
+                }
                 vec3 dir = v3(0, 0, 0);
                 if (c <= nl) {
                     const float u1 = u01(win_at(w, j + 1));
                     const float u2 = u01(win_at(w, j + 2));
                     k += 3;
                     if (c < nl) {
-                        dir = light_sample_dir(kp.lights[c], tpos, u1, u2);
+                        dir = light_sample_dir(LS.light(c), tpos, u1, u2);
                         if (COUNT) ++c_lsamp;
                     } else {
                         dir = frame_apply(tfr, cosine_sample_local(u1, u2));
@@ -300,11 +382,11 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(KParams kp) {
             vec3 li_pos = v3(0, 0, 0);
             float li_pow = 0.0f;
             for (int l = 0; l < nl; ++l) {
-                const LightDev& L = kp.lights[l];
+                const LightDev& L = LS.light(l);
                 vec3 hp;
                 const bool h = light_trace(L, ro, rd, &hp);
                 if (COUNT) c_ltr += (is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u);
-                if (is_iter) lmix += kp.weights[l] * light_pdf(L, ro, h, hp);
+                if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp);
                 if (h && (!has_li || length(li_pos - ro) > length(hp - ro))) {
                     has_li = true;
                     li_pos = hp;
@@ -635,21 +717,26 @@ int needed_susp(const ipt_params* p) {
     return maxpush < 0 ? 0 : maxpush;  // suspended levels = depth of deepest pushed node
 }
 
-template <int MAXSUSP>
-int launch_path(ipt_ctx* ctx, const KParams& kp, hipStream_t st, bool count) {
-    const size_t lds = (size_t)MAXSUSP * kStackFields * kBlock * sizeof(float) + 60 * sizeof(float);
+template <int MAXSUSP, bool COUNT, int LMODE>
+int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
+    const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words()) * sizeof(float);
     const int blocks_per_cu = lds * 2 <= 160 * 1024 ? 2 : 1;
     dim3 grid(ctx->n_cu * blocks_per_cu), block(kBlock);
-    HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, true>,
+    HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, COUNT, LMODE>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, false>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (count)
-        hipLaunchKernelGGL((path_kernel<MAXSUSP, true>), grid, block, lds, st, kp);
-    else
-        hipLaunchKernelGGL((path_kernel<MAXSUSP, false>), grid, block, lds, st, kp);
+    hipLaunchKernelGGL((path_kernel<MAXSUSP, COUNT, LMODE>), grid, block, lds, st, kp);
     HIPCHECK(ctx, hipGetLastError());
     return IPT_OK;
+}
+template <int MAXSUSP, bool COUNT>
+int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
+    if (kp.n_lights == 1) return launch_path3<MAXSUSP, COUNT, kLightsOne>(ctx, kp, st);
+    if (kp.n_lights <= kLdsLights) return launch_path3<MAXSUSP, COUNT, kLightsLds>(ctx, kp, st);
+    return launch_path3<MAXSUSP, COUNT, kLightsGlobal>(ctx, kp, st);
+}
+template <int MAXSUSP>
+int launch_path(ipt_ctx* ctx, const KParams& kp, hipStream_t st, bool count) {
+    return count ? launch_path2<MAXSUSP, true>(ctx, kp, st) : launch_path2<MAXSUSP, false>(ctx, kp, st);
 }
 
 int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t st,
@@ -710,8 +797,6 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
         if (susp <= 4)
             rc = launch_path<4>(ctx, kp, st, count);
-        else if (susp <= 6)
-            rc = launch_path<6>(ctx, kp, st, count);
         else if (susp <= 8)
             rc = launch_path<8>(ctx, kp, st, count);
         else

@@ -400,8 +400,13 @@ IPT_HD float acos_f64_to_f32(float x) { return (float)acos_d_((double)x); }
 // 0x358637be; float(1e-6) = 0x358637bd < 1e-6).
 IPT_HD bool lt_1em6(float f) { return f < u2f(0x358637beu); }
 
-// CosineDdf::value (ddf.cpp:232-238): (float)((double)z / M_PI)
-IPT_HD float div_pi_to_f32(float z) { return (float)((double)z / u2d(0x400921fb54442d18ull)); }
+// CosineDdf::value (ddf.cpp:232-238): (float)((double)z / M_PI).
+// For every float z in [0, 2], (float)(z * (double)(1/M_PI)) rounds to the
+// same float as the f64 quotient (checked exhaustively against host libm in
+// tests/test_math_exhaustive.py::test_mixed_precision_helpers), so the f64
+// division is a multiply. The reference only reaches z in [0, 1+2^-22]
+// (z = (inverse*d).z with |d| = 1 and an orthonormal inverse).
+IPT_HD float div_pi_to_f32(float z) { return (float)((double)z * u2d(0x3fd45f306dc9c883ull)); }
 
 // CosineDdf::sample phi (ddf.cpp:228): (float)(2*M_PI*(double)u2)
 IPT_HD float two_pi_times(float u) { return (float)(u2d(0x401921fb54442d18ull) * (double)u); }
