@@ -34,7 +34,7 @@ using namespace ipt;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kStackFields = 18;  // pos3, frame12, res, mult, i
+constexpr int kStackFields = 6;   // pos3, res, mult, meta(i | kind<<8)
 constexpr int kPoolChunk = 256;   // work units per global atomic
 constexpr int kNumCounters = 11;
 
@@ -58,7 +58,7 @@ struct KParams {
     const Frame* __restrict__ wall_frames;  // [5]
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int n_spheres;
-    const float4* spheres;   // (c.xyz, r)
+    const float4* __restrict__ spheres;   // (c.xyz, r)
 };
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
@@ -90,9 +90,8 @@ __device__ __forceinline__ void philox_fill(uint32_t& d0, uint32_t& d1, uint32_t
 }
 
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
-// r=0.5 sphere, 6 an extra sphere (center in *sc), -1 miss.
-__device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim,
-                                                vec3* sc) {
+// r=0.5 sphere, 6+i extra sphere i, -1 miss.
+__device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim) {
     if (kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
     // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
     int p;
@@ -103,8 +102,7 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
         float t = sphere_t(s.w, o - c, d);
         if (isfinite_(t) && gt_1em6(fabs_(t)) && t < best) {
             best = t;
-            p = 6;
-            *sc = c;
+            p = 6 + i;
         }
     }
     *prim = p;
@@ -154,7 +152,7 @@ struct LightSet {
 };
 
 template <int MAXSUSP, bool COUNT, int LMODE>
-__global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
+__global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
     float* wallf = lds + MAXSUSP * kStackFields * kBlock;     // [5][12]
@@ -197,20 +195,26 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
     const int nl = kp.n_lights;
     const float w_sdf = kp.weights[nl];
     const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
+    // n at every depth is n_rays >> d; when n_rays is a power of two, res/n ==
+    // res * 2^-e exactly (both round the same exact quotient)
+    const bool n_pow2 = kp.n_rays > 0 && (kp.n_rays & (kp.n_rays - 1)) == 0;
+    const int n_log2 = n_pow2 ? 31 - __clz(kp.n_rays) : 0;
 
     // wave-local unit pool (uniform)
     unsigned long long pool_next = 0, pool_end = 0;
 
-    // lane state
-    bool active = true, has_path = false;
+    // lane state. The current node lives in registers; suspended ancestors in
+    // LDS as {pos.xyz, res, pending multiplier, meta = i | kind<<8}. Frames are
+    // never stored: walls load theirs from the LDS table, sphere nodes rebuild
+    // theirs (make_frame) in the frame phase of the step after a push or pop.
+    bool active = true, has_path = false, fresh = false, need_frame = false, need_b = false;
     unsigned long long unit = 0;
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
     vec3 tpos = v3(0, 0, 0);
     Frame tfr;
     float tres = 0.0f;
-    int ti = 0, tdepth = 0;
-    int dest_x = 0, dest_y = 0;
+    int ti = 0, tdepth = 0, tkind = 0;  // kind: 0..4 wall plane, 5 box sphere, 6+i extra sphere i
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
              c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0;
 
@@ -244,20 +248,69 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
                 } else {
                     unit = my;
                     has_path = true;
-                    tdepth = -1;  // marks "camera ray pending"
+                    fresh = true;
                 }
             }
         }
         if (__ballot(active) == 0) break;
 
-        // -------------------------------------------------- advance phase
+        // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
+        if (active && has_path && !fresh) {
+            for (;;) {
+                const int n = kp.n_rays >> tdepth;
+                if (ti < n) break;
+                float v = 0.0f;
+                if (isfinite_(tres))
+                    v = n_pow2 ? tres * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - tdepth))
+                               : tres / (float)n;
+                if (tdepth == 0) {
+                    kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
+                    has_path = false;
+                    break;
+                }
+                const int lvl = tdepth - 1;
+                const float* b = stk + (size_t)lvl * kStackFields * kBlock + tid;
+                tpos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
+                const float pres = b[3 * kBlock];
+                const float pmult = b[4 * kBlock];
+                const int meta = __float_as_int(b[5 * kBlock]);
+                tres = pres + (pmult * 1.0f) * v;  // res += multiplier*albedo*ray_power
+                ti = meta & 0xff;
+                tkind = meta >> 8;
+                tdepth = lvl;
+                if (tkind < 5) {
+                    const float* f = wallf + tkind * 12;
+                    tfr.m0 = v3(f[0], f[1], f[2]);
+                    tfr.m1 = v3(f[3], f[4], f[5]);
+                    tfr.m2 = v3(f[6], f[7], f[8]);
+                    tfr.iz = v3(f[9], f[10], f[11]);
+                    need_frame = false;
+                } else {
+                    need_frame = true;
+                }
+            }
+        }
+
+        // ---------------------- phase 2: RotateDdf of sphere nodes (ddf_detail.h:73-84)
+        if (need_frame && has_path) {
+            vec3 nrm;
+            if (tkind == 5) {
+                nrm = normalize(tpos);  // GeometrySphereInBox.cpp:67
+            } else {
+                const float4 sp = kp.spheres[tkind - 6];
+                nrm = normalize(tpos - v3(sp.x, sp.y, sp.z));  // FractalSpheres.cpp:91
+            }
+            tfr = make_frame(nrm);
+        }
+        need_frame = false;
+
+        // ------------------------------------ phase 3: camera ray or one iteration
         bool have_ray = false, is_iter = false;
         vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         int rdepth = 0;
-        float sdf_val = 0.0f;
-
-        if (active && has_path && tdepth == -1) {
+        if (active && has_path && fresh) {
             // new path: render_sample pixel body (main.cpp:192-211)
+            fresh = false;
             const unsigned long long s = unit / per_pass;
             const unsigned long long rem = unit - s * per_pass;
             const int cand = (int)(rem / (unsigned long long)kp.W);
@@ -272,8 +325,8 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
             rpass = (uint32_t)(kp.spp_offset + (int)s);
             rpix = (uint32_t)(iy * kp.W + ix);
             philox_fill(w.a0, w.a1, w.a2, w.a3, 0u, rpass, rpix, kp.key0, kp.key1);
-            philox_fill(w.b0, w.b1, w.b2, w.b3, 1u, rpass, rpix, kp.key0, kp.key1);
             blk = 0;
+            need_b = true;  // block 1 is produced by the window refill of the next iteration
             k = 2;
             const float x = jitter_coord(ix, u01(w.a0), kp.W);
             const float y = jitter_coord(iy, u01(w.a1), kp.H);
@@ -284,9 +337,6 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
             uint8_t code = 0xff;
             if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < kp.W && yi < kp.H)
                 code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
-            kp.codes[unit] = code;
-            dest_x = xi;
-            dest_y = yi;
             if (code != 0x05 && code != 0xff) {
                 kp.flags[(size_t)yn * kp.W + ix] = 1;
                 kp.flags[(size_t)yi * kp.W + xi] = 1;
@@ -295,9 +345,10 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
             if (code == 0xff || !owned_row(kp, yi)) {
                 // not ours (halo row of another shard) or out of range
                 kp.values[unit] = 0.0f;
-                if (code != 0xff) kp.codes[unit] = 0xfe;
+                kp.codes[unit] = code == 0xff ? code : (uint8_t)0xfe;
                 has_path = false;
             } else {
+                kp.codes[unit] = code;
                 ro = kp.cam_pos;
                 rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
                 rdepth = 0;
@@ -305,75 +356,53 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
                 if (COUNT) ++c_paths;
             }
         } else if (active && has_path) {
-            // finalize finished nodes (main.cpp:181) and pop (main.cpp:177)
-            for (;;) {
-                const int n = kp.n_rays >> tdepth;
-                if (ti < n) break;
-                const float v = isfinite_(tres) ? tres / (float)n : 0.0f;
-                if (tdepth == 0) {
-                    const float val = v >= 0.0f ? v : 0.0f;  // main.cpp:214
-                    kp.values[unit] = val;
-                    has_path = false;
-                    break;
-                }
-                const int lvl = tdepth - 1;
-                float* b = stk + (size_t)lvl * kStackFields * kBlock + tid;
-                tpos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
-                tfr.m0 = v3(b[3 * kBlock], b[4 * kBlock], b[5 * kBlock]);
-                tfr.m1 = v3(b[6 * kBlock], b[7 * kBlock], b[8 * kBlock]);
-                tfr.m2 = v3(b[9 * kBlock], b[10 * kBlock], b[11 * kBlock]);
-                tfr.iz = v3(b[12 * kBlock], b[13 * kBlock], b[14 * kBlock]);
-                const float pres = b[15 * kBlock];
-                const float pmult = b[16 * kBlock];
-                ti = __float_as_int(b[17 * kBlock]);
-                tres = pres + (pmult * 1.0f) * v;  // res += multiplier*albedo*ray_power
-                tdepth = lvl;
+            // one iteration of the branch loop (main.cpp:149-178)
+            if ((k >> 2) != blk) {
+                w.a0 = w.b0; w.a1 = w.b1; w.a2 = w.b2; w.a3 = w.b3;
+                ++blk;
+                need_b = true;
             }
-            if (has_path) {
-                // one iteration of the branch loop (main.cpp:149-178)
-                if ((k >> 2) != blk) {
-                    w.a0 = w.b0; w.a1 = w.b1; w.a2 = w.b2; w.a3 = w.b3;
-                    ++blk;
-                    philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
-                }
-                const uint32_t j = k - 4 * blk;
-                const float r = u01(win_at(w, j));
-                // UnionDdf::sample pick (ddf.cpp:142-153): first c with r < cdf[c]
-                int c = 0;
-                if (LMODE == kLightsOne) {
-                    c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+            if (need_b) {
+                philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
+                need_b = false;
+            }
+            const uint32_t j = k - 4 * blk;
+            const float r = u01(win_at(w, j));
+            // UnionDdf::sample pick (ddf.cpp:142-153): first c with r < cdf[c]
+            int c = 0;
+            if (LMODE == kLightsOne) {
+                c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+            } else {
+                while (c <= nl && !(r < LS.cdf(c))) ++c;
+            }
+            vec3 dir = v3(0, 0, 0);
+            if (c <= nl) {
+                const float u1 = u01(win_at(w, j + 1));
+                const float u2 = u01(win_at(w, j + 2));
+                k += 3;
+                if (c < nl) {
+                    dir = light_sample_dir(LS.light(c), tpos, u1, u2);
+                    if (COUNT) ++c_lsamp;
                 } else {
-                    while (c <= nl && !(r < LS.cdf(c))) ++c;
+                    dir = frame_apply(tfr, cosine_sample_local(u1, u2));
                 }
-                vec3 dir = v3(0, 0, 0);
-                if (c <= nl) {
-                    const float u1 = u01(win_at(w, j + 1));
-                    const float u2 = u01(win_at(w, j + 2));
-                    k += 3;
-                    if (c < nl) {
-                        dir = light_sample_dir(LS.light(c), tpos, u1, u2);
-                        if (COUNT) ++c_lsamp;
-                    } else {
-                        dir = frame_apply(tfr, cosine_sample_local(u1, u2));
-                    }
-                } else {
-                    k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
-                }
-                ++ti;
-                if (COUNT) ++c_iter;
-                if (is_zero(dir)) {
-                    if (COUNT) ++c_skip;
-                } else {
-                    ro = tpos;
-                    rd = dir;
-                    rdepth = tdepth + 1;
-                    have_ray = true;
-                    is_iter = true;
-                }
+            } else {
+                k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
+            }
+            ++ti;
+            if (COUNT) ++c_iter;
+            if (is_zero(dir)) {
+                if (COUNT) ++c_skip;
+            } else {
+                ro = tpos;
+                rd = dir;
+                rdepth = tdepth + 1;
+                have_ray = true;
+                is_iter = true;
             }
         }
 
-        // -------------------------------------------------- trace phase
+        // --------------------------------------------- phase 4: trace + resolve
         if (have_ray) {
             // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
             // and the child's CollectionLighting::traceRayToLight
@@ -395,17 +424,17 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
             }
             float mult = 0.0f;
             if (is_iter) {
-                sdf_val = frame_cosine_value(tfr, rd);
+                const float sdf_val = frame_cosine_value(tfr, rd);
                 const float mix = lmix + w_sdf * sdf_val;
                 mult = sdf_val / mix;
             }
             // child ray_power (main.cpp:100-143)
             float cv = 0.0f;
             bool push = false;
-            vec3 si_pos = v3(0, 0, 0), sph_c = v3(0, 0, 0);
+            vec3 si_pos = v3(0, 0, 0);
             int prim = -1;
             if (rdepth < kp.depth_max) {
-                const float t = trace_geometry(kp, ro, rd, &prim, &sph_c);
+                const float t = trace_geometry(kp, ro, rd, &prim);
                 const bool has_si = prim >= 0;
                 if (COUNT) {
                     ++c_traced;
@@ -431,16 +460,15 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
             if (push) {
                 if (is_iter) {
                     float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
-                    b[0 * kBlock] = tpos.x; b[1 * kBlock] = tpos.y; b[2 * kBlock] = tpos.z;
-                    b[3 * kBlock] = tfr.m0.x; b[4 * kBlock] = tfr.m0.y; b[5 * kBlock] = tfr.m0.z;
-                    b[6 * kBlock] = tfr.m1.x; b[7 * kBlock] = tfr.m1.y; b[8 * kBlock] = tfr.m1.z;
-                    b[9 * kBlock] = tfr.m2.x; b[10 * kBlock] = tfr.m2.y; b[11 * kBlock] = tfr.m2.z;
-                    b[12 * kBlock] = tfr.iz.x; b[13 * kBlock] = tfr.iz.y; b[14 * kBlock] = tfr.iz.z;
-                    b[15 * kBlock] = tres;
-                    b[16 * kBlock] = mult;
-                    b[17 * kBlock] = __int_as_float(ti);
+                    b[0 * kBlock] = tpos.x;
+                    b[1 * kBlock] = tpos.y;
+                    b[2 * kBlock] = tpos.z;
+                    b[3 * kBlock] = tres;
+                    b[4 * kBlock] = mult;
+                    b[5 * kBlock] = __int_as_float(ti | (tkind << 8));
                 }
                 tpos = si_pos;
+                tkind = prim;
                 if (prim < 5) {
                     const float* f = wallf + prim * 12;
                     tfr.m0 = v3(f[0], f[1], f[2]);
@@ -448,8 +476,7 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
                     tfr.m2 = v3(f[6], f[7], f[8]);
                     tfr.iz = v3(f[9], f[10], f[11]);
                 } else {
-                    const vec3 nrm = prim == 5 ? normalize(si_pos) : normalize(si_pos - sph_c);
-                    tfr = make_frame(nrm);
+                    need_frame = true;  // built in phase 2 of the next step
                     if (COUNT) ++c_sframe;
                 }
                 tres = 0.0f;
@@ -459,8 +486,7 @@ __global__ __launch_bounds__(kBlock, 2) void path_kernel(const KParams kp) {
                 tres = tres + (mult * 1.0f) * cv;
             } else {
                 // the camera ray itself ended (light, miss, depth_max or n_rays==0)
-                const float val = cv >= 0.0f ? cv : 0.0f;
-                kp.values[unit] = val;
+                kp.values[unit] = cv >= 0.0f ? cv : 0.0f;
                 has_path = false;
             }
         }
@@ -618,6 +644,7 @@ struct ipt_ctx {
     unsigned long long* d_counters = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
+    int blocks_per_cu = 0;
 };
 
 namespace {
@@ -720,10 +747,16 @@ int needed_susp(const ipt_params* p) {
 template <int MAXSUSP, bool COUNT, int LMODE>
 int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words()) * sizeof(float);
-    const int blocks_per_cu = lds * 2 <= 160 * 1024 ? 2 : 1;
-    dim3 grid(ctx->n_cu * blocks_per_cu), block(kBlock);
     HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, COUNT, LMODE>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // persistent grid: every block the CUs can hold at once (a work queue, no
+    // inter-block waits, so an over-reported residency only queues blocks)
+    int bpc = 0;
+    HIPCHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                      &bpc, (const void*)path_kernel<MAXSUSP, COUNT, LMODE>, kBlock, lds));
+    bpc = std::max(1, std::min(bpc, 8));
+    ctx->blocks_per_cu = bpc;
+    dim3 grid(ctx->n_cu * bpc), block(kBlock);
     hipLaunchKernelGGL((path_kernel<MAXSUSP, COUNT, LMODE>), grid, block, lds, st, kp);
     HIPCHECK(ctx, hipGetLastError());
     return IPT_OK;
