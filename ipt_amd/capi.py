@@ -96,7 +96,7 @@ def load(path: str | os.PathLike | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("IPT_LIB_PATH", LIB_PATH))
     if not p.exists():
         raise IptError(IPT_E_DEVICE, f"{p} is not built; run __graft_entry__.build()")
     lib = C.CDLL(str(p))

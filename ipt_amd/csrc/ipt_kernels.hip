@@ -34,6 +34,18 @@ using namespace ipt;
 namespace {
 
 constexpr int kBlock = 256;
+
+// Profiling-only builds (-DIPT_ABL=n, scripts/ablate.sh): phase n is computed a
+// second time on a perturbed input and kept alive, so the wall-time delta is
+// that phase's marginal cost with the path tree unchanged. 0 in the product.
+#ifndef IPT_ABL
+#define IPT_ABL 0
+#endif
+template <typename T>
+__device__ __forceinline__ void keep_alive(const T& v) {
+    const float* p = reinterpret_cast<const float*>(&v);
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) asm volatile("" ::"v"(p[i]));
+}
 constexpr int kStackFields = 6;   // pos3, res, mult, meta(i | kind<<8)
 constexpr int kPoolChunk = 256;   // work units per global atomic
 constexpr int kNumCounters = 11;
@@ -59,6 +71,7 @@ struct KParams {
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int n_spheres;
     const float4* __restrict__ spheres;   // (c.xyz, r)
+    float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
@@ -114,9 +127,11 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
 // the candidate-row table live in LDS after the DFS stack.
 constexpr int kLdsLights = 16;
 constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
-constexpr int kLdsCand = 1024;
+constexpr int kLdsCand = 512;
+constexpr int kFrameSlots = 128;  // sphere-frame builds per workgroup step (overflow retries)
 __host__ __device__ constexpr size_t scene_lds_words() {
-    return 60 + (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) + kLdsCand;
+    return 60 + (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) + kLdsCand + 4 +
+           12 * kFrameSlots + 3 * kBlock;
 }
 
 // Where the lights live during the step loop (compile time, so that no
@@ -160,7 +175,12 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
     float* weights_lds = wallf + 60 + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
     int* cand_lds = reinterpret_cast<int*>(cdf_lds + (kLdsLights + 1));
+    int* xcnt = cand_lds + kLdsCand;                          // [2 parities][frames, cosines]
+    float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [12][kFrameSlots]
+    float* xcos = xfr + 12 * kFrameSlots;                      // [3][kBlock]
     const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    if (tid < 4) xcnt[tid] = 0;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
     const bool cand_in_lds = sharded && kp.n_cand <= kLdsCand;
     if (tid < 60) wallf[tid] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
@@ -208,6 +228,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
     // never stored: walls load theirs from the LDS table, sphere nodes rebuild
     // theirs (make_frame) in the frame phase of the step after a push or pop.
     bool active = true, has_path = false, fresh = false, need_frame = false, need_b = false;
+    uint32_t step = 0;
     unsigned long long unit = 0;
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
@@ -252,7 +273,6 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 }
             }
         }
-        if (__ballot(active) == 0) break;
 
         // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
         if (active && has_path && !fresh) {
@@ -291,25 +311,11 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             }
         }
 
-        // ---------------------- phase 2: RotateDdf of sphere nodes (ddf_detail.h:73-84)
-        if (need_frame && has_path) {
-            vec3 nrm;
-            if (tkind == 5) {
-                nrm = normalize(tpos);  // GeometrySphereInBox.cpp:67
-            } else {
-                const float4 sp = kp.spheres[tkind - 6];
-                nrm = normalize(tpos - v3(sp.x, sp.y, sp.z));  // FractalSpheres.cpp:91
-            }
-            tfr = make_frame(nrm);
-        }
-        need_frame = false;
-
-        // ------------------------------------ phase 3: camera ray or one iteration
+        // ------------------------- phase 2: new path (render_sample body, main.cpp:192-211)
         bool have_ray = false, is_iter = false;
         vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         int rdepth = 0;
         if (active && has_path && fresh) {
-            // new path: render_sample pixel body (main.cpp:192-211)
             fresh = false;
             const unsigned long long s = unit / per_pass;
             const unsigned long long rem = unit - s * per_pass;
@@ -351,12 +357,52 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 kp.codes[unit] = code;
                 ro = kp.cam_pos;
                 rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
+                if (IPT_ABL == 6) {
+                    uint32_t q0, q1, q2, q3;
+                    philox_fill(q0, q1, q2, q3, (uint32_t)kp.abl_zero, rpass, rpix, kp.key0, kp.key1);
+                    keep_alive(q0 ^ q1);
+                    keep_alive(camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x + kp.abl_zero, y));
+                }
                 rdepth = 0;
                 have_ray = true;
                 if (COUNT) ++c_paths;
             }
-        } else if (active && has_path) {
-            // one iteration of the branch loop (main.cpp:149-178)
+        }
+
+        // ------------- phase 3: post the step's expensive, divergent tasks to the
+        // workgroup (RotateDdf frames of sphere nodes, CosineDdf local samples) so
+        // that they run on ceil(N/64) dense wave-passes instead of on every wave.
+        const int par = step & 1;
+        bool want_frame = need_frame && has_path;
+        int slot_f = 0;
+        {
+            const uint64_t m = __ballot(want_frame);
+            if (m) {
+                const int first = __ffsll((long long)m) - 1;
+                int base = 0;
+                if (lane == first) base = atomicAdd(&xcnt[par * 2 + 0], __popcll(m));
+                base = __shfl(base, first);
+                slot_f = base + __popcll(m & lanemask_lt);
+            }
+        }
+        const bool stalled = want_frame && slot_f >= kFrameSlots;  // retry next step
+        if (want_frame && !stalled) {
+            vec3 nrm;
+            if (tkind == 5) {
+                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67 (done by the worker)
+            } else {
+                const float4 sp = kp.spheres[tkind - 6];
+                nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
+            }
+            xfr[0 * kFrameSlots + slot_f] = nrm.x;
+            xfr[1 * kFrameSlots + slot_f] = nrm.y;
+            xfr[2 * kFrameSlots + slot_f] = nrm.z;
+        }
+        // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
+        const bool iter_lane = active && has_path && !have_ray && !stalled;
+        int pick = -1;
+        float u1 = 0.0f, u2 = 0.0f;
+        if (iter_lane) {
             if ((k >> 2) != blk) {
                 w.a0 = w.b0; w.a1 = w.b1; w.a2 = w.b2; w.a3 = w.b3;
                 ++blk;
@@ -364,30 +410,105 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             }
             if (need_b) {
                 philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
+                if (IPT_ABL == 3) {
+                    uint32_t q0, q1, q2, q3;
+                    philox_fill(q0, q1, q2, q3, blk + 1 + (uint32_t)kp.abl_zero, rpass, rpix, kp.key0, kp.key1);
+                    keep_alive(q0 ^ q1 ^ q2 ^ q3);
+                }
                 need_b = false;
             }
             const uint32_t j = k - 4 * blk;
             const float r = u01(win_at(w, j));
-            // UnionDdf::sample pick (ddf.cpp:142-153): first c with r < cdf[c]
             int c = 0;
             if (LMODE == kLightsOne) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
             } else {
                 while (c <= nl && !(r < LS.cdf(c))) ++c;
             }
-            vec3 dir = v3(0, 0, 0);
+            pick = c;
             if (c <= nl) {
-                const float u1 = u01(win_at(w, j + 1));
-                const float u2 = u01(win_at(w, j + 2));
+                u1 = u01(win_at(w, j + 1));
+                u2 = u01(win_at(w, j + 2));
                 k += 3;
-                if (c < nl) {
-                    dir = light_sample_dir(LS.light(c), tpos, u1, u2);
-                    if (COUNT) ++c_lsamp;
-                } else {
-                    dir = frame_apply(tfr, cosine_sample_local(u1, u2));
-                }
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
+            }
+        }
+        const bool want_cos = iter_lane && pick == nl;
+        int slot_c = 0;
+        {
+            const uint64_t m = __ballot(want_cos);
+            if (m) {
+                const int first = __ffsll((long long)m) - 1;
+                int base = 0;
+                if (lane == first) base = atomicAdd(&xcnt[par * 2 + 1], __popcll(m));
+                base = __shfl(base, first);
+                slot_c = base + __popcll(m & lanemask_lt);
+            }
+        }
+        if (want_cos) {
+            xcos[0 * kBlock + slot_c] = u1;
+            xcos[1 * kBlock + slot_c] = u2;
+        }
+        // barrier A; also the block-wide exit test (every wave runs every barrier)
+        if (!__syncthreads_or(active ? 1 : 0)) break;
+        if (tid == 0) {
+            xcnt[(1 - par) * 2 + 0] = 0;
+            xcnt[(1 - par) * 2 + 1] = 0;
+        }
+        {
+            const int nf = min(xcnt[par * 2 + 0], kFrameSlots);
+            const int nc = xcnt[par * 2 + 1];
+            const int pf = (nf + 63) >> 6, pc = (nc + 63) >> 6;
+            // passes dealt round-robin to the 4 waves, frames from wave 0 up and
+            // cosine samples from wave 3 down, so a single busy wave is rare
+            for (int pass = wave; pass < pf + pc; pass += kBlock / 64) {
+                if (pass < pf) {
+                    const int sl = pass * 64 + lane;
+                    if (sl < nf) {
+                        const vec3 nn = normalize(v3(xfr[0 * kFrameSlots + sl], xfr[1 * kFrameSlots + sl],
+                                                     xfr[2 * kFrameSlots + sl]));
+                        const Frame f = make_frame(nn);
+                        if (IPT_ABL == 1) keep_alive(make_frame(nn * (1.0f + kp.abl_zero)));
+                        xfr[0 * kFrameSlots + sl] = f.m0.x; xfr[1 * kFrameSlots + sl] = f.m0.y;
+                        xfr[2 * kFrameSlots + sl] = f.m0.z; xfr[3 * kFrameSlots + sl] = f.m1.x;
+                        xfr[4 * kFrameSlots + sl] = f.m1.y; xfr[5 * kFrameSlots + sl] = f.m1.z;
+                        xfr[6 * kFrameSlots + sl] = f.m2.x; xfr[7 * kFrameSlots + sl] = f.m2.y;
+                        xfr[8 * kFrameSlots + sl] = f.m2.z; xfr[9 * kFrameSlots + sl] = f.iz.x;
+                        xfr[10 * kFrameSlots + sl] = f.iz.y; xfr[11 * kFrameSlots + sl] = f.iz.z;
+                    }
+                } else {
+                    const int sl = (pc - 1 - (pass - pf)) * 64 + lane;
+                    if (sl < nc) {
+                        const vec3 v = cosine_sample_local(xcos[0 * kBlock + sl], xcos[1 * kBlock + sl]);
+                        if (IPT_ABL == 2)
+                            keep_alive(cosine_sample_local(xcos[0 * kBlock + sl] + kp.abl_zero, xcos[1 * kBlock + sl]));
+                        xcos[0 * kBlock + sl] = v.x;
+                        xcos[1 * kBlock + sl] = v.y;
+                        xcos[2 * kBlock + sl] = v.z;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // barrier B: results visible
+        if (want_frame && !stalled) {
+            tfr.m0 = v3(xfr[0 * kFrameSlots + slot_f], xfr[1 * kFrameSlots + slot_f], xfr[2 * kFrameSlots + slot_f]);
+            tfr.m1 = v3(xfr[3 * kFrameSlots + slot_f], xfr[4 * kFrameSlots + slot_f], xfr[5 * kFrameSlots + slot_f]);
+            tfr.m2 = v3(xfr[6 * kFrameSlots + slot_f], xfr[7 * kFrameSlots + slot_f], xfr[8 * kFrameSlots + slot_f]);
+            tfr.iz = v3(xfr[9 * kFrameSlots + slot_f], xfr[10 * kFrameSlots + slot_f], xfr[11 * kFrameSlots + slot_f]);
+            need_frame = false;
+        }
+
+        // ------------------------- phase 3b: the iteration's direction (main.cpp:149-163)
+        if (iter_lane) {
+            vec3 dir = v3(0, 0, 0);
+            if (pick < nl) {
+                dir = light_sample_dir(LS.light(pick), tpos, u1, u2);
+                if (IPT_ABL == 7) keep_alive(light_sample_dir(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
+                if (COUNT) ++c_lsamp;
+            } else if (pick == nl) {
+                dir = frame_apply(tfr, v3(xcos[0 * kBlock + slot_c], xcos[1 * kBlock + slot_c],
+                                          xcos[2 * kBlock + slot_c]));
             }
             ++ti;
             if (COUNT) ++c_iter;
@@ -401,6 +522,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 is_iter = true;
             }
         }
+        ++step;
 
         // --------------------------------------------- phase 4: trace + resolve
         if (have_ray) {
@@ -414,6 +536,11 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 const LightDev& L = LS.light(l);
                 vec3 hp;
                 const bool h = light_trace(L, ro, rd, &hp);
+                if (IPT_ABL == 4) {
+                    vec3 hq;
+                    const bool h2 = light_trace(L, ro, rd * (1.0f + kp.abl_zero), &hq);
+                    keep_alive(light_pdf(L, ro, h2, hq));
+                }
                 if (COUNT) c_ltr += (is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u);
                 if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp);
                 if (h && (!has_li || length(li_pos - ro) > length(hp - ro))) {
@@ -435,6 +562,11 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             int prim = -1;
             if (rdepth < kp.depth_max) {
                 const float t = trace_geometry(kp, ro, rd, &prim);
+                if (IPT_ABL == 5) {
+                    int p2;
+                    keep_alive(trace_geometry(kp, ro, rd * (1.0f + kp.abl_zero), &p2));
+                    keep_alive(p2);
+                }
                 const bool has_si = prim >= 0;
                 if (COUNT) {
                     ++c_traced;

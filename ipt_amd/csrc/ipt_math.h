@@ -116,6 +116,10 @@ IPT_HD mat3 inverse(const mat3& M) {
 // ------------------------------------------------------------------ acosf
 // glibc 2.35 sysdeps/ieee754/flt-32/e_acosf.c (fdlibm), constants verified
 // against libm.so.6 .rodata (0x9c958..0x9c98c).
+// Branch-free over fdlibm's three argument ranges: every lane evaluates the
+// exact operation sequence of its own branch (selects only pick results), so
+// the value is the glibc one while a wave pays one division/sqrt chain, not
+// three (the |x|<0.5 and x>0.5 ranges both occur within every wave).
 IPT_HD float acosf_(float x) {
     const float one = 1.0f;
     const float pi = u2f(0x40490fdau);
@@ -128,38 +132,23 @@ IPT_HD float acosf_(float x) {
                 qS4 = u2f(0x3d9dc62eu);
     const uint32_t hx = f2u(x);
     const uint32_t ix = hx & 0x7fffffffu;
-    if (ix == 0x3f800000u) {
-        if ((int32_t)hx > 0) return 0.0f;
-        return pi + two_pio2_lo;
-    } else if (ix > 0x3f800000u) {
-        return (x - x) / (x - x);
-    }
-    if (ix < 0x3f000000u) {  // |x| < 0.5
-        if (ix <= 0x32800000u) return pio2_hi + pio2_lo;
-        float z = x * x;
-        float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        float r = p / q;
-        return pio2_hi - (x - (pio2_lo - x * r));
-    } else if ((int32_t)hx < 0) {  // x < -0.5
-        float z = (one + x) * 0.5f;
-        float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        float s = sqrt_(z);
-        float r = p / q;
-        float w = r * s - pio2_lo;
-        return pi - 2.0f * (s + w);
-    } else {  // x > 0.5
-        float z = (one - x) * 0.5f;
-        float s = sqrt_(z);
-        float df = u2f(f2u(s) & 0xfffff000u);
-        float c = (z - df * df) / (s + df);
-        float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        float r = p / q;
-        float w = r * s + c;
-        return 2.0f * (df + w);
-    }
+    const bool small = ix < 0x3f000000u;  // |x| < 0.5
+    const bool neg = (int32_t)hx < 0;     // x < -0.5 when !small
+    const float z = small ? x * x : (neg ? (one + x) * 0.5f : (one - x) * 0.5f);
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    const float sq = sqrt_(z);
+    const float r_small = pio2_hi - (x - (pio2_lo - x * r));
+    const float r_neg = pi - 2.0f * (sq + (r * sq - pio2_lo));
+    const float df = u2f(f2u(sq) & 0xfffff000u);
+    const float c = (z - df * df) / (sq + df);
+    const float r_pos = 2.0f * (df + (r * sq + c));
+    float res = small ? r_small : (neg ? r_neg : r_pos);
+    if (small && ix <= 0x32800000u) res = pio2_hi + pio2_lo;
+    if (ix == 0x3f800000u) res = (int32_t)hx > 0 ? 0.0f : pi + two_pio2_lo;
+    if (ix > 0x3f800000u) res = (x - x) * inf_();  // |x|>1 or NaN: NaN
+    return res;
 }
 
 // ------------------------------------------------------------ sinf / cosf
@@ -236,20 +225,13 @@ IPT_HD double reduce_fast_(double x, int* np) {
     return fma_(-(double)n, u2d(0x3ff921fb54442d18ull), x);
 }
 
+IPT_HD void sincosf_small_(float y, float* sp, float* cp);
 IPT_HD float sinf_(float y) {
     double x = y;
-    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {  // pio4
-        double s = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sin_poly_(x, s, sincos_table(0));
-    } else if (abstop12(y) < abstop12(120.0f)) {
-        int n;
-        x = reduce_fast_(x, &n);
-        double s = sincos_sign(n & 3);
-        sincos_tab p = sincos_table((n & 2) ? 1 : 0);
-        double x2 = x * x;
-        if ((n & 1) == 0) return sin_poly_(x * s, x2, p);
-        return cos_poly_(x2, p);
+    if (abstop12(y) < abstop12(120.0f)) {
+        float sv, cv;
+        sincosf_small_(y, &sv, &cv);
+        return sv;
     } else if (abstop12(y) < abstop12(u2f(0x7f800000u))) {
         uint32_t xi = f2u(y);
         int sign = xi >> 31;
@@ -266,18 +248,10 @@ IPT_HD float sinf_(float y) {
 
 IPT_HD float cosf_(float y) {
     double x = y;
-    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {
-        double x2 = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
-        return cos_poly_(x2, sincos_table(0));
-    } else if (abstop12(y) < abstop12(120.0f)) {
-        int n;
-        x = reduce_fast_(x, &n);
-        double s = sincos_sign(n & 3);
-        sincos_tab p = sincos_table((n & 2) ? 1 : 0);
-        double x2 = x * x;
-        if (n & 1) return sin_poly_(x * s, x2, p);
-        return cos_poly_(x2, p);
+    if (abstop12(y) < abstop12(120.0f)) {
+        float sv, cv;
+        sincosf_small_(y, &sv, &cv);
+        return cv;
     } else if (abstop12(y) < abstop12(u2f(0x7f800000u))) {
         uint32_t xi = f2u(y);
         int sign = xi >> 31;
@@ -297,24 +271,20 @@ IPT_HD float cosf_(float y) {
 // CosineDdf angles in [0,pi/2] and [0,2pi)). Equal bit-for-bit to
 // sinf_/cosf_ there (glibc's __sincosf_fma SLP-vectorises the same FMA graph;
 // tests/test_math_exhaustive.py checks the equality against host sincosf).
+// Branch-free: for |y| < pi/4 glibc skips the reduction, but reduce_fast_
+// then yields n = 0 and x - 0*hpi == x exactly (fma with a -0 product), i.e.
+// the same polynomial inputs; only |y| < 2^-12 needs a select.
 IPT_HD void sincosf_small_(float y, float* sp, float* cp) {
-    double x = y;
-    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {
-        double x2 = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) { *sp = y; *cp = 1.0f; return; }
-        sincos_tab p = sincos_table(0);
-        *sp = sin_poly_(x, x2, p);
-        *cp = cos_poly_(x2, p);
-        return;
-    }
     int n;
-    x = reduce_fast_(x, &n);
-    double s = sincos_sign(n & 3);
-    sincos_tab p = sincos_table((n & 2) ? 1 : 0);
-    double x2 = x * x;
-    float a = sin_poly_(x * s, x2, p);
-    float b = cos_poly_(x2, p);
-    if (n & 1) { *sp = b; *cp = a; } else { *sp = a; *cp = b; }
+    const double x = reduce_fast_((double)y, &n);
+    const double s = sincos_sign(n & 3);
+    const sincos_tab p = sincos_table((n & 2) ? 1 : 0);
+    const double x2 = x * x;
+    const float a = sin_poly_(x * s, x2, p);
+    const float b = cos_poly_(x2, p);
+    const bool tiny = abstop12(y) < abstop12(0x1p-12f);
+    *sp = tiny ? y : ((n & 1) ? b : a);
+    *cp = tiny ? 1.0f : ((n & 1) ? a : b);
 }
 IPT_HD void sincosf_(float y, float* sp, float* cp) {
     if (abstop12(y) < abstop12(120.0f)) {
@@ -324,21 +294,11 @@ IPT_HD void sincosf_(float y, float* sp, float* cp) {
     *sp = sinf_(y);
     *cp = cosf_(y);
 }
-// sinf for |y| < 120 (same code path as sinf_ there)
+// sinf for |y| < 120 (same arithmetic as sinf_ there)
 IPT_HD float sinf_small_(float y) {
-    double x = y;
-    if (abstop12(y) < abstop12(0.785398185253143310546875f)) {
-        double s = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return y;
-        return sin_poly_(x, s, sincos_table(0));
-    }
-    int n;
-    x = reduce_fast_(x, &n);
-    double s = sincos_sign(n & 3);
-    sincos_tab p = sincos_table((n & 2) ? 1 : 0);
-    double x2 = x * x;
-    if ((n & 1) == 0) return sin_poly_(x * s, x2, p);
-    return cos_poly_(x2, p);
+    float sv, cv;
+    sincosf_small_(y, &sv, &cv);
+    return sv;
 }
 
 // ------------------------------------------------- (float)acos((double)x)
@@ -357,39 +317,28 @@ IPT_HD double acos_d_(double x) {
     const uint64_t hx64 = d2u(x);
     const uint32_t hx = (uint32_t)(hx64 >> 32);
     const uint32_t ix = hx & 0x7fffffffu;
+    // branch-free over fdlibm's three ranges (see acosf_)
+    const bool small = ix < 0x3fe00000u;
+    const bool neg = (int32_t)hx < 0;
+    const double z = small ? x * x : (neg ? (1.0 + x) * 0.5 : (1.0 - x) * 0.5);
+    const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const double r = p / q;
+    const double sq = sqrtd_(z);
+    const double r_small = pio2_hi - (x - (pio2_lo - x * r));
+    const double r_neg = pi - 2.0 * (sq + (r * sq - pio2_lo));
+    const double df = u2d(d2u(sq) & 0xffffffff00000000ull);
+    const double c = (z - df * df) / (sq + df);
+    const double r_pos = 2.0 * (df + (r * sq + c));
+    double res = small ? r_small : (neg ? r_neg : r_pos);
+    if (small && ix <= 0x3c600000u) res = pio2_hi + pio2_lo;
     if (ix >= 0x3ff00000u) {
-        if (((ix - 0x3ff00000u) | (uint32_t)hx64) == 0) {
-            if ((int32_t)hx > 0) return 0.0;
-            return pi + 2.0 * pio2_lo;
-        }
-        return (x - x) / (x - x);
+        if (((ix - 0x3ff00000u) | (uint32_t)hx64) == 0)
+            res = (int32_t)hx > 0 ? 0.0 : pi + 2.0 * pio2_lo;
+        else
+            res = (x - x) * (double)inf_();
     }
-    if (ix < 0x3fe00000u) {
-        if (ix <= 0x3c600000u) return pio2_hi + pio2_lo;
-        double z = x * x;
-        double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        double r = p / q;
-        return pio2_hi - (x - (pio2_lo - x * r));
-    } else if ((int32_t)hx < 0) {
-        double z = (1.0 + x) * 0.5;
-        double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        double s = sqrtd_(z);
-        double r = p / q;
-        double w = r * s - pio2_lo;
-        return pi - 2.0 * (s + w);
-    } else {
-        double z = (1.0 - x) * 0.5;
-        double s = sqrtd_(z);
-        double df = u2d(d2u(s) & 0xffffffff00000000ull);
-        double c = (z - df * df) / (s + df);
-        double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        double r = p / q;
-        double w = r * s + c;
-        return 2.0 * (df + w);
-    }
+    return res;
 }
 IPT_HD float acos_f64_to_f32(float x) { return (float)acos_d_((double)x); }
 
