@@ -30,14 +30,26 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 
+# BASELINE.json configs: (scene, width, per-rank height, spp per step, steps)
+CONFIGS = {
+    "c2": ("box", 1024, 1024, 32, 8),       # configs[1]: 1024^2, 256 spp, 8 bounces (the metric)
+    "c3": ("spheres10k", 1024, 1024, 1, 4),  # configs[2]: 10k spheres (64 spp in full; sampled)
+    "c4": ("box", 4096, 4096, 8, 4),         # configs[3]: 4096^2 tiles across GPUs (1024 spp in full)
+    "c5": ("lights256", 2048, 2048, 2, 4),   # configs[4]: 256 emitters, 2048^2 (512 spp in full)
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload: c2 (default, the metric's config), c3 10k "
+                         "spheres, c4 4096^2 multi-GPU, c5 256 emitters")
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp-per-step", type=int, default=32)
-    ap.add_argument("--width", type=int, default=1024)
-    ap.add_argument("--height", type=int, default=1024, help="per-rank share of frame rows")
+    ap.add_argument("--spp-per-step", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None, help="per-rank share of frame rows")
     ap.add_argument("--n-rays", type=int, default=16)
     ap.add_argument("--depth-max", type=int, default=8)
     ap.add_argument("--seed", type=int, default=20241223)
@@ -47,7 +59,26 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-counters", action="store_true",
                     help="skip the (untimed) counting re-render used for the roofline")
-    return ap.parse_args()
+    a = ap.parse_args()
+    scene, w, h, spp, steps = CONFIGS[a.config]
+    a.scene = scene
+    a.width = a.width or w
+    a.height = a.height or h
+    a.spp_per_step = a.spp_per_step or spp
+    a.steps = a.steps or steps
+    return a
+
+
+def make_desc(name):
+    from ipt_amd import scenes
+
+    if name == "box":
+        return scenes.make_scene_box()
+    if name == "lights256":
+        return scenes.make_scene_box_lights(16)
+    if name == "spheres10k":
+        return scenes.make_scene_spheres(10000, seed=1)
+    raise ValueError(name)
 
 
 def cpu_baseline(args, desc):
@@ -114,7 +145,7 @@ def main():
 
     from ipt_amd import capi, roofline, scenes
 
-    desc = scenes.make_scene_box()
+    desc = make_desc(args.scene)
     ctx = capi.Context(local_rank)
     ctx.upload_scene(desc)
 
@@ -192,7 +223,7 @@ def main():
             ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64, device=dev)
             dist.all_reduce(ct)
             cnt = dict(zip(capi.COUNTER_NAMES, [int(x) for x in ct.tolist()]))
-        ops = roofline.ops_from_counters(cnt)
+        ops = roofline.ops_from_counters(cnt, n_spheres=len(desc.get("spheres", [])))
         # per launch on one rank: ops/world per launch, average launch duration
         launch_s = path_ms / 1e3 / args.steps
         achieved = ops / world / args.steps / launch_s
@@ -224,6 +255,10 @@ def main():
             "traffic_source": traffic_src,
             "kernel": "path_kernel",
             "ops_per_path": ops / cnt["paths"],
+            "bvh_nodes_per_trace": (cnt["bvh_nodes"] / max(cnt["traced_rays"], 1)) if desc.get("spheres") else None,
+            "sphere_tests_per_trace": (cnt["sphere_tests"] / max(cnt["traced_rays"], 1)) if desc.get("spheres") else None,
+            "reference_scan_ops_per_path": (roofline.reference_scan_ops(cnt, len(desc["spheres"])) / cnt["paths"]
+                                            if desc.get("spheres") else None),
             "launch_ms": launch_s * 1e3,
             "note": ("algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
                      "counters) per launch / HIP-event launch time; VALU issue peak "
@@ -242,7 +277,7 @@ def main():
         }
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.config == "c2":
         try:
             cpu = cpu_baseline(args, desc)
         except Exception as e:  # the GPU number stands on its own
@@ -262,8 +297,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (sample_scenes[0] geometry/light/camera, Philox per-path RNG)",
-            "config": {"workload": f"sample_scenes[0] {W}x{H}, {spp_total} spp, depth_max "
-                                   f"{args.depth_max}, n_rays {args.n_rays}",
+            "config": {"workload": f"{args.config}: {args.scene} {W}x{H}, {spp_total} spp, "
+                                   f"depth_max {args.depth_max}, n_rays {args.n_rays}",
+                       "baseline_config": args.config,
                        "width": W, "height": H, "spp": spp_total,
                        "spp_per_step": args.spp_per_step, "depth_max": args.depth_max,
                        "n_rays": args.n_rays, "tile_rows": args.tile_rows if world > 1 else 0,

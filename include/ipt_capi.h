@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IPT_ABI_VERSION 1
+#define IPT_ABI_VERSION 2
 
 enum {
     IPT_OK = 0,
@@ -132,6 +132,8 @@ typedef struct ipt_counters {
     uint64_t sphere_frames;   /* RotateDdf builds at non-wall normals */
     uint64_t light_traces;    /* AreaLight::traceRay calls */
     uint64_t drifted;         /* samples GridRenderPlane maps off their nominal pixel */
+    uint64_t bvh_nodes;       /* sphere-BVH nodes visited (IPT_GEOM_SPHERES_IN_BOX) */
+    uint64_t sphere_tests;    /* intersection_with_sphere evaluations on the sphere list */
 } ipt_counters;
 
 typedef struct ipt_ctx ipt_ctx;

@@ -63,9 +63,11 @@ class Image(C.Structure):
                 ("pixel_max", C.c_void_p)]
 
 
+ABI_VERSION = 2  # include/ipt_capi.h IPT_ABI_VERSION
+
 COUNTER_NAMES = ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
                  "iterations", "light_samples", "skipped", "sphere_frames", "light_traces",
-                 "drifted")
+                 "drifted", "bvh_nodes", "sphere_tests")
 
 
 class Counters(C.Structure):
@@ -101,6 +103,8 @@ def load(path: str | os.PathLike | None = None):
         raise IptError(IPT_E_DEVICE, f"{p} is not built; run __graft_entry__.build()")
     lib = C.CDLL(str(p))
     lib.ipt_abi_version.restype = C.c_int
+    if lib.ipt_abi_version() != ABI_VERSION:
+        raise IptError(IPT_E_INVALID, f"{p}: ABI {lib.ipt_abi_version()} != {ABI_VERSION}; rebuild")
     lib.ipt_last_error.restype = C.c_char_p
     lib.ipt_last_error.argtypes = [C.c_void_p]
     lib.ipt_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/ipt_capi.h"
+#include "ipt_bvh.h"
 #include "ipt_path.h"
 
 using namespace ipt;
@@ -48,7 +49,7 @@ __device__ __forceinline__ void keep_alive(const T& v) {
 }
 constexpr int kStackFields = 6;   // pos3, res, mult, meta(i | kind<<8)
 constexpr int kPoolChunk = 256;   // work units per global atomic
-constexpr int kNumCounters = 11;
+constexpr int kNumCounters = 13;
 
 struct KParams {
     int W, H, spp, spp_offset, n_rays, depth_max;
@@ -71,6 +72,9 @@ struct KParams {
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int n_spheres;
     const float4* __restrict__ spheres;   // (c.xyz, r)
+    const BvhNode* __restrict__ bvh_nodes;     // n_nodes > 0: sphere BVH (ipt_bvh.h)
+    const BvhSphere* __restrict__ bvh_prims;
+    int n_nodes;
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
@@ -102,23 +106,75 @@ __device__ __forceinline__ void philox_fill(uint32_t& d0, uint32_t& d1, uint32_t
     d3 = o.v[3];
 }
 
+// Conservative slab test (entry distance or +inf). Approximate reciprocals
+// are fine here: only whether a subtree can contain the scan's winner is
+// decided, with margins; the winner itself comes from the exact sphere_t().
+__device__ __forceinline__ float bvh_box_entry(const BvhNode& b, vec3 o, vec3 inv) {
+    const float tx0 = (b.bmin[0] - o.x) * inv.x, tx1 = (b.bmax[0] - o.x) * inv.x;
+    const float ty0 = (b.bmin[1] - o.y) * inv.y, ty1 = (b.bmax[1] - o.y) * inv.y;
+    const float tz0 = (b.bmin[2] - o.z) * inv.z, tz1 = (b.bmax[2] - o.z) * inv.z;
+    const float tnear = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tfar = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return tnear <= tfar * 1.0001f + 1e-5f ? tnear : inf_();
+}
+__device__ __forceinline__ float safe_rcp(float d) {
+    return d == 0.0f ? (f2u(d) >> 31 ? -1e30f : 1e30f) : __builtin_amdgcn_rcpf(d);
+}
+
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
-// r=0.5 sphere, 6+i extra sphere i, -1 miss.
-__device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim) {
+// r=0.5 sphere, 6+i extra sphere i (original index), -1 miss.
+template <bool COUNT>
+__device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim, uint32_t& c_nodes,
+                                                uint32_t& c_tests) {
     if (kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
     // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
+    // (FractalSpheres.cpp:75-84): strict '<' in index order == minimal t,
+    // lowest index among equal t, and a sphere never wins a tie with a plane.
     int p;
     float best = trace_box_planes_only(o, d, &p);
-    for (int i = 0; i < kp.n_spheres; ++i) {
-        float4 s = kp.spheres[i];
-        vec3 c = v3(s.x, s.y, s.z);
-        float t = sphere_t(s.w, o - c, d);
-        if (isfinite_(t) && gt_1em6(fabs_(t)) && t < best) {
-            best = t;
-            p = 6 + i;
+    int bidx = -1;
+    if (kp.n_nodes > 0) {
+        const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+        // near-child-first linearisation for this direction octant (ipt_bvh.h)
+        const int oct = (int)(f2u(d.x) >> 31) | (int)(f2u(d.y) >> 31) << 1 | (int)(f2u(d.z) >> 31) << 2;
+        const BvhNode* __restrict__ nodes = kp.bvh_nodes + (size_t)oct * kp.n_nodes;
+        int i = 0;
+        while (i < kp.n_nodes) {
+            const BvhNode nd = nodes[i];
+            if (COUNT) ++c_nodes;
+            const float te = bvh_box_entry(nd, o, inv);
+            // te == inf is a miss; it must not pass when best is inf too (open floor)
+            const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f;
+            if (enter && nd.leaf >= 0) {
+                const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
+                if (COUNT) c_tests += (uint32_t)cnt;
+                for (int k2 = 0; k2 < cnt; ++k2) {
+                    const BvhSphere sp = kp.bvh_prims[first + k2];
+                    const float t = sphere_t(sp.r, o - v3(sp.c[0], sp.c[1], sp.c[2]), d);
+                    if (isfinite_(t) && gt_1em6(fabs_(t)) &&
+                        (t < best || (t == best && bidx >= 0 && sp.index < bidx))) {
+                        best = t;
+                        bidx = sp.index;
+                    }
+                }
+                i = nd.skip;
+            } else {
+                i = enter ? i + 1 : nd.skip;
+            }
+        }
+    } else {
+        if (COUNT) c_tests += (uint32_t)kp.n_spheres;
+        for (int i = 0; i < kp.n_spheres; ++i) {
+            float4 s = kp.spheres[i];
+            vec3 c = v3(s.x, s.y, s.z);
+            float t = sphere_t(s.w, o - c, d);
+            if (isfinite_(t) && gt_1em6(fabs_(t)) && t < best) {
+                best = t;
+                bidx = i;
+            }
         }
     }
-    *prim = p;
+    *prim = bidx >= 0 ? 6 + bidx : p;
     return best;
 }
 
@@ -237,7 +293,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
     float tres = 0.0f;
     int ti = 0, tdepth = 0, tkind = 0;  // kind: 0..4 wall plane, 5 box sphere, 6+i extra sphere i
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
-             c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0;
+             c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0, c_nodes = 0, c_tests = 0;
 
     for (;;) {
         // -------------------------------------------------- unit refill
@@ -561,10 +617,10 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             vec3 si_pos = v3(0, 0, 0);
             int prim = -1;
             if (rdepth < kp.depth_max) {
-                const float t = trace_geometry(kp, ro, rd, &prim);
+                const float t = trace_geometry<COUNT>(kp, ro, rd, &prim, c_nodes, c_tests);
                 if (IPT_ABL == 5) {
                     int p2;
-                    keep_alive(trace_geometry(kp, ro, rd * (1.0f + kp.abl_zero), &p2));
+                    keep_alive(trace_geometry<false>(kp, ro, rd * (1.0f + kp.abl_zero), &p2, c_nodes, c_tests));
                     keep_alive(p2);
                 }
                 const bool has_si = prim >= 0;
@@ -636,6 +692,8 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
         atomicAdd(&kp.counters[8], (unsigned long long)c_sframe);
         atomicAdd(&kp.counters[9], (unsigned long long)c_ltr);
         atomicAdd(&kp.counters[10], (unsigned long long)c_drift);
+        atomicAdd(&kp.counters[11], (unsigned long long)c_nodes);
+        atomicAdd(&kp.counters[12], (unsigned long long)c_tests);
     }
 }
 
@@ -762,6 +820,9 @@ struct ipt_ctx {
     Frame* d_wall = nullptr;
     float4* d_spheres = nullptr;
     int n_spheres = 0;
+    BvhNode* d_bvh_nodes = nullptr;
+    BvhSphere* d_bvh_prims = nullptr;
+    int n_nodes = 0;
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     // work buffers
     float* d_values = nullptr;
@@ -957,6 +1018,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cam_up = ctx->cam_up;
         kp.n_spheres = ctx->n_spheres;
         kp.spheres = ctx->d_spheres;
+        kp.bvh_nodes = ctx->d_bvh_nodes;
+        kp.bvh_prims = ctx->d_bvh_prims;
+        kp.n_nodes = ctx->n_nodes;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
         HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
@@ -1052,7 +1116,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
 void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
+    void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters};
     for (void* b : bufs)
@@ -1099,12 +1163,28 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     std::vector<float4> sph(std::max(s->n_spheres, 1));
     for (int i = 0; i < s->n_spheres; ++i)
         sph[i] = make_float4(s->spheres[i].center[0], s->spheres[i].center[1], s->spheres[i].center[2], s->spheres[i].radius);
-    void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres};
+    std::vector<BvhNode> bnodes;
+    std::vector<BvhSphere> bprims;
+    int per_order = 0;
+    if (s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX && s->n_spheres > 16)
+        bvh_build(reinterpret_cast<const float*>(sph.data()), s->n_spheres, bnodes, bprims, &per_order);
+    void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes,
+                   ctx->d_bvh_prims};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_lights = nullptr;
     ctx->d_weights = ctx->d_cdf = nullptr;
     ctx->d_spheres = nullptr;
+    ctx->d_bvh_nodes = nullptr;
+    ctx->d_bvh_prims = nullptr;
+    ctx->n_nodes = 0;
+    if (!bnodes.empty()) {
+        HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_nodes, sizeof(BvhNode) * bnodes.size()));
+        HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_prims, sizeof(BvhSphere) * bprims.size()));
+        HIPCHECK(ctx, hipMemcpy(ctx->d_bvh_nodes, bnodes.data(), sizeof(BvhNode) * bnodes.size(), hipMemcpyHostToDevice));
+        HIPCHECK(ctx, hipMemcpy(ctx->d_bvh_prims, bprims.data(), sizeof(BvhSphere) * bprims.size(), hipMemcpyHostToDevice));
+        ctx->n_nodes = per_order;  // nodes per octant order; buffer holds kBvhOrders of them
+    }
     HIPCHECK(ctx, hipMalloc(&ctx->d_lights, sizeof(LightDev) * L.size()));
     HIPCHECK(ctx, hipMalloc(&ctx->d_weights, sizeof(float) * (nl + 1)));
     HIPCHECK(ctx, hipMalloc(&ctx->d_cdf, sizeof(float) * (nl + 1)));
@@ -1204,6 +1284,8 @@ int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
     out->sphere_frames = h[8];
     out->light_traces = h[9];
     out->drifted = h[10];
+    out->bvh_nodes = h[11];
+    out->sphere_tests = h[12];
     return IPT_OK;
 }
 

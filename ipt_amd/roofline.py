@@ -30,12 +30,17 @@ OPS = {
     "iter_cosine": 118,      # cosine-sampled branch iteration
     "iter_skipped": 56,      # skipped (back-facing light sample)
     "node_finalize": 1,
+    "sphere_test": 37,       # intersection_with_sphere + FractalSpheres acceptance
+    "bvh_node": 29,          # slab test + entry/prune compares, per BVH node visited
 }
 TRANSC = {"rotate_build": 3, "iter_cosine": 4}
 
 
-def ops_from_counters(c: dict) -> float:
-    """Algorithmic op-eq for a set of ipt_counters (box-family scenes)."""
+def ops_from_counters(c: dict, n_spheres: int = 0) -> float:
+    """Algorithmic op-eq for a set of ipt_counters. The base formula is §8(d)'s
+    for sample_scenes[0]; many-light scenes add 57 per AreaLight::traceRay
+    beyond the box's two per traced ray, sphere-stress scenes add 37 per
+    sphere test (§8(d): "C3 adds N x 37 per trace")."""
     kept_light = c["light_samples"] - c["skipped"]
     cosine = c["iterations"] - c["light_samples"]
     f = (c["paths"] * OPS["camera"]
@@ -48,7 +53,17 @@ def ops_from_counters(c: dict) -> float:
          + cosine * (OPS["iter_cosine"] + TRANSC["iter_cosine"] * TRANSC_OP_EQ)
          + c["skipped"] * OPS["iter_skipped"]
          + c["expanded_nodes"] * OPS["node_finalize"])
+    f += max(0, c["light_traces"] - 2 * c["traced_rays"]) * OPS["light_trace"]
+    if "sphere_tests" in c:
+        f += c["sphere_tests"] * OPS["sphere_test"] + c.get("bvh_nodes", 0) * OPS["bvh_node"]
+    else:
+        f += c["traced_rays"] * n_spheres * OPS["sphere_test"]
     return float(f)
+
+
+def reference_scan_ops(c: dict, n_spheres: int) -> float:
+    """Op-eq of the reference's brute-force sphere scan for the same rays."""
+    return float(c["traced_rays"]) * n_spheres * OPS["sphere_test"]
 
 
 def accumulate_bytes(n_dest_pixels: int, spp: int, with_sums: bool = True,

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     lib = capi.load()
     for s in declared_symbols():
         assert hasattr(lib, s)
-    assert lib.ipt_abi_version() == 1
+    assert lib.ipt_abi_version() == capi.ABI_VERSION
 
 
 def test_no_cpu_fallback():

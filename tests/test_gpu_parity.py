@@ -111,3 +111,35 @@ def test_sharded_render_matches_whole_frame(gpu_ctx, oracle, n_shards):
     for k in ("pixels", "sums", "pixel_max"):
         assert np.array_equal(_bits(acc[k]), _bits(whole[k])), k
     assert np.array_equal(acc["counters"], whole["counters"])
+
+
+@pytest.mark.parametrize("k", [2, 4, 16])
+def test_many_lights_bit_exact(gpu_ctx, oracle, k):
+    """BASELINE configs[4] scene family: the [0] light split into k x k
+    co-planar squares (k=16: 256 emitters, global-memory light mode)."""
+    desc = scenes.make_scene_box_lights(k)
+    p = capi.make_params(24, 20, 2, n_rays=16, depth_max=8)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+def test_spheres_in_box_c3_scene(gpu_ctx, oracle):
+    """The full 10k-sphere scene of BASELINE configs[2] (bench C3): BVH walk
+    (octant orders, open-floor rays with best = inf) against the oracle's scan."""
+    desc = scenes.make_scene_spheres(10000, seed=1)
+    p = capi.make_params(12, 10, 1, n_rays=8, depth_max=4)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+@pytest.mark.parametrize("n", [1, 50, 400, 3000])
+def test_spheres_in_box_bit_exact(gpu_ctx, oracle, n):
+    """BASELINE configs[2] scene family: box planes + n seeded spheres with
+    FractalSpheres' acceptance rule."""
+    desc = scenes.make_scene_spheres(n, seed=1)
+    p = capi.make_params(20, 16, 1, n_rays=16, depth_max=8)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
