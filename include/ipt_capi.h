@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IPT_ABI_VERSION 2
+#define IPT_ABI_VERSION 3
 
 enum {
     IPT_OK = 0,
@@ -134,6 +134,8 @@ typedef struct ipt_counters {
     uint64_t drifted;         /* samples GridRenderPlane maps off their nominal pixel */
     uint64_t bvh_nodes;       /* sphere-BVH nodes visited (IPT_GEOM_SPHERES_IN_BOX) */
     uint64_t sphere_tests;    /* intersection_with_sphere evaluations on the sphere list */
+    uint64_t light_nodes;     /* light-BVH nodes visited (many-light scenes) */
+    uint64_t light_tests;     /* AreaLight::traceRay evaluations actually run */
 } ipt_counters;
 
 typedef struct ipt_ctx ipt_ctx;

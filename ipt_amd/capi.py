@@ -63,11 +63,11 @@ class Image(C.Structure):
                 ("pixel_max", C.c_void_p)]
 
 
-ABI_VERSION = 2  # include/ipt_capi.h IPT_ABI_VERSION
+ABI_VERSION = 3  # include/ipt_capi.h IPT_ABI_VERSION
 
 COUNTER_NAMES = ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
                  "iterations", "light_samples", "skipped", "sphere_frames", "light_traces",
-                 "drifted", "bvh_nodes", "sphere_tests")
+                 "drifted", "bvh_nodes", "sphere_tests", "light_nodes", "light_tests")
 
 
 class Counters(C.Structure):

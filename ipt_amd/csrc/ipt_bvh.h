@@ -1,19 +1,38 @@
-// ipt_bvh.h — exact-result acceleration for the sphere-list geometry
-// (IPT_GEOM_SPHERES_IN_BOX, BASELINE configs[2]).
+// ipt_bvh.h — exact-result acceleration structures for the two O(N) scans on
+// the path: the sphere list (IPT_GEOM_SPHERES_IN_BOX, BASELINE configs[2],
+// FractalSpheres.cpp:75-84) and the light list (CollectionLighting.cpp:23-34
+// and UnionDdf::value over its lights, ddf.cpp:157-162; configs with L=256).
 //
-// The reference scans every sphere (FractalSpheres.cpp:75-84) and keeps the
-// first sphere whose t is the strict minimum. A BVH returns the same sphere
-// iff (1) no sphere that the scan would accept is pruned and (2) ties on t are
-// broken by the lowest original index. (1) holds because every node box is
-// the union of its spheres' boxes padded by a relative margin far above the
-// rounding error of sphere_t's hit point, and a subtree is skipped on its
-// entry distance only with a margin; (2) is enforced explicitly. The exact
-// per-sphere test is the same sphere_t() the brute-force path uses, so the
-// result is bit-identical (tests/test_gpu_parity.py::test_spheres_in_box_*).
+// A BVH returns the scan's result iff no item that the scan would accept is
+// skipped, and ties are resolved as the scan resolves them.
+//
+// * Conservativeness. Every item box is padded so that any ray the exact
+//   per-item test (sphere_t / light_trace, the same functions the scans use)
+//   accepts passes through the padded box, rounding included. The padding is
+//   derived from a bound D on |origin - item| (ray origins are the camera or
+//   surface points of the scene, both known at upload):
+//     sphere: the float discriminant 4b^2 - 4(|oc|^2 - r^2) carries an
+//       absolute error below ~1e-6 D^2 (dot products, squares, |d| != 1), so a
+//       ray whose distance to the centre is up to sqrt(r^2 + 4e-6 D^2) may be
+//       accepted; near tangency the computed t moves by up to sqrt(4e-6) D / 2
+//       = 1e-3 D along the ray. pad = (sqrt(r^2 + 4e-6 D^2) - r) + 1e-3 D
+//       + 1e-4 (|c| + r + 1).
+//     light: the hit point o + d t and coord = inv * rel carry errors of a few
+//       ulps of D plus cond(M) ulps of the light extent. pad = 1e-5 D
+//       + 1e-4 (|P| + |x| + |y| + 1) + 1e-5 cond (|x| + |y|); ill-conditioned
+//       (cond > 1e4) or non-finite lights disable the light BVH.
+//   The slab test itself uses approximate reciprocals with a relative margin.
+// * Ties. Spheres: the walk can meet them in any order, so equal t is broken
+//   by the lowest original index (the scan's first-strict-minimum). Lights:
+//   the tree is built over contiguous INDEX ranges, so its depth-first walk
+//   meets lights in increasing index order and the scan's running compare and
+//   running sum are reproduced operation for operation; a light the walk skips
+//   would have contributed exactly +0 to the sum and nothing to the nearest
+//   hit.
 //
 // Layout: nodes in depth-first order with skip links (stackless traversal):
 // an inner node's first child is the next node; `skip` is the node after its
-// subtree. Leaves reference a contiguous range of the reordered sphere array.
+// subtree. Leaves reference a contiguous range of items.
 #pragma once
 
 #include <algorithm>
@@ -29,7 +48,7 @@ struct BvhNode {
     float bmin[3];
     int skip;   // next node index when this subtree is done or missed
     float bmax[3];
-    int leaf;   // -1: inner; else first sphere index (reordered) | count << 24
+    int leaf;   // -1: inner; else first item | count << 24
 };
 
 struct BvhSphere {
@@ -39,17 +58,21 @@ struct BvhSphere {
     int pad[3];
 };
 
-// Host builder: median split on the widest axis, leaves of <= 4 spheres.
-// The tree is emitted as kBvhOrders = 8 depth-first linearisations, one per
-// ray-direction octant (bit a set = direction negative along axis a): at every
-// inner node the child on the near side of the split axis comes first, so the
-// stackless walk meets near hits early and prunes the rest on `best`. The
-// order only changes how much is visited, never the result (tie-break above).
-constexpr int kBvhOrders = 8;
-inline void bvh_build(const float* cr /* [n][4] c.xyz r */, int n, std::vector<BvhNode>& nodes,
-                      std::vector<BvhSphere>& prims, int* nodes_per_order) {
+struct BvhBox {
+    float lo[3], hi[3];
+};
+
+// Binary tree over items [0, n) with item boxes `box`. spatial: median split
+// of box centres on the widest axis (items permuted, `perm` = original index
+// per slot); otherwise split the index range in half (perm = identity, leaves
+// in index order). Emits `orders` depth-first linearisations of
+// nodes_per_order nodes each: with orders == 8, linearisation `oct` (bit a set
+// = ray direction negative on axis a) puts the near child first at every node.
+inline void bvh_build_boxes(const std::vector<BvhBox>& box, int leaf_size, bool spatial, int orders,
+                            std::vector<BvhNode>& nodes, std::vector<int>& perm, int* nodes_per_order) {
+    const int n = (int)box.size();
     nodes.clear();
-    prims.clear();
+    perm.clear();
     *nodes_per_order = 0;
     if (n <= 0) return;
     struct TreeNode {
@@ -59,41 +82,22 @@ inline void bvh_build(const float* cr /* [n][4] c.xyz r */, int n, std::vector<B
     std::vector<TreeNode> tree;
     std::vector<int> idx(n);
     for (int i = 0; i < n; ++i) idx[i] = i;
-    auto sphere_box = [&](int i, float* lo, float* hi) {
-        const float r = cr[4 * i + 3];
-        for (int a = 0; a < 3; ++a) {
-            const float c = cr[4 * i + a];
-            // relative + absolute padding: >> the float error of o + d*t
-            const float pad = 1e-4f * (std::fabs(c) + r + 1.0f);
-            lo[a] = c - r - pad;
-            hi[a] = c + r + pad;
-        }
-    };
     std::function<int(int, int)> rec = [&](int lo, int hi) -> int {
         TreeNode tn{};
         for (int a = 0; a < 3; ++a) {
             tn.lo[a] = INFINITY;
             tn.hi[a] = -INFINITY;
         }
-        for (int k = lo; k < hi; ++k) {
-            float l[3], h[3];
-            sphere_box(idx[k], l, h);
+        for (int k = lo; k < hi; ++k)
             for (int a = 0; a < 3; ++a) {
-                tn.lo[a] = std::min(tn.lo[a], l[a]);
-                tn.hi[a] = std::max(tn.hi[a], h[a]);
+                tn.lo[a] = std::min(tn.lo[a], box[idx[k]].lo[a]);
+                tn.hi[a] = std::max(tn.hi[a], box[idx[k]].hi[a]);
             }
-        }
         const int me = (int)tree.size();
         tree.push_back(tn);
-        if (hi - lo <= 4) {
-            tree[me].leaf = (int)prims.size() | ((hi - lo) << 24);
-            for (int k = lo; k < hi; ++k) {
-                BvhSphere s{};
-                for (int a = 0; a < 3; ++a) s.c[a] = cr[4 * idx[k] + a];
-                s.r = cr[4 * idx[k] + 3];
-                s.index = idx[k];
-                prims.push_back(s);
-            }
+        if (hi - lo <= leaf_size) {
+            tree[me].leaf = (int)perm.size() | ((hi - lo) << 24);
+            for (int k = lo; k < hi; ++k) perm.push_back(idx[k]);
             return me;
         }
         int axis = 0;
@@ -104,9 +108,11 @@ inline void bvh_build(const float* cr /* [n][4] c.xyz r */, int n, std::vector<B
                 axis = a;
             }
         const int mid = (lo + hi) / 2;
-        std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi,
-                         [&](int x, int y) { return cr[4 * x + axis] < cr[4 * y + axis]; });
-        const int c0 = rec(lo, mid);  // lower half along axis
+        if (spatial)
+            std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi, [&](int x, int y) {
+                return box[x].lo[axis] + box[x].hi[axis] < box[y].lo[axis] + box[y].hi[axis];
+            });
+        const int c0 = rec(lo, mid);  // lower half (along axis, or of the index range)
         const int c1 = rec(mid, hi);
         tree[me].leaf = -1;
         tree[me].axis = axis;
@@ -117,8 +123,8 @@ inline void bvh_build(const float* cr /* [n][4] c.xyz r */, int n, std::vector<B
     rec(0, n);
     const int per = (int)tree.size();
     *nodes_per_order = per;
-    nodes.resize((size_t)per * kBvhOrders);
-    for (int oct = 0; oct < kBvhOrders; ++oct) {
+    nodes.resize((size_t)per * orders);
+    for (int oct = 0; oct < orders; ++oct) {
         BvhNode* out = nodes.data() + (size_t)per * oct;
         int next = 0;
         std::function<void(int)> emit = [&](int k) {
@@ -130,7 +136,8 @@ inline void bvh_build(const float* cr /* [n][4] c.xyz r */, int n, std::vector<B
             }
             out[me].leaf = tn.leaf;
             if (tn.leaf < 0) {
-                const int neg = (oct >> tn.axis) & 1;  // negative direction: upper half first
+                // negative direction along the split axis: upper half first
+                const int neg = (spatial && orders == 8) ? (oct >> tn.axis) & 1 : 0;
                 emit(tn.child[neg]);
                 emit(tn.child[1 - neg]);
             }
@@ -138,6 +145,95 @@ inline void bvh_build(const float* cr /* [n][4] c.xyz r */, int n, std::vector<B
         };
         emit(0);
     }
+}
+
+// Bound on |origin - p| for every ray origin of the scene and every point p
+// of an item box [lo, hi]: origins are the camera or surface points in [-B, B]^3.
+inline double origin_bound(const float cam[3], float B, const float lo[3], const float hi[3]) {
+    double dc = 0.0, db = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double e1 = std::max(std::fabs((double)cam[a] - lo[a]), std::fabs((double)cam[a] - hi[a]));
+        const double e2 = (double)B + std::max(std::fabs((double)lo[a]), std::fabs((double)hi[a]));
+        dc += e1 * e1;
+        db += e2 * e2;
+    }
+    return std::sqrt(std::max(dc, db));
+}
+
+constexpr int kBvhOrders = 8;
+
+// Sphere BVH (8 octant orders, leaves of <= 4 spheres). cr: [n][4] c.xyz r.
+inline void bvh_build_spheres(const float* cr, int n, const float cam[3], float B, std::vector<BvhNode>& nodes,
+                              std::vector<BvhSphere>& prims, int* nodes_per_order) {
+    std::vector<BvhBox> box(n);
+    for (int i = 0; i < n; ++i) {
+        const float r = cr[4 * i + 3];
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = cr[4 * i + a] - r;
+            hi[a] = cr[4 * i + a] + r;
+        }
+        const double D = origin_bound(cam, B, lo, hi);
+        const double cn = std::fabs((double)cr[4 * i]) + std::fabs((double)cr[4 * i + 1]) +
+                          std::fabs((double)cr[4 * i + 2]);
+        const double pad = (std::sqrt((double)r * r + 4e-6 * D * D) - r) + 1e-3 * D + 1e-4 * (cn + r + 1.0);
+        for (int a = 0; a < 3; ++a) {
+            box[i].lo[a] = (float)((double)lo[a] - pad);
+            box[i].hi[a] = (float)((double)hi[a] + pad);
+        }
+    }
+    std::vector<int> perm;
+    bvh_build_boxes(box, 4, true, kBvhOrders, nodes, perm, nodes_per_order);
+    prims.resize(perm.size());
+    for (size_t k = 0; k < perm.size(); ++k) {
+        const int i = perm[k];
+        BvhSphere s{};
+        for (int a = 0; a < 3; ++a) s.c[a] = cr[4 * i + a];
+        s.r = cr[4 * i + 3];
+        s.index = i;
+        prims[k] = s;
+    }
+}
+
+// Light BVH over index ranges (one order, leaves of <= 2 lights, items in
+// index order). P, x, y: corner and axes; inv: inverse(mat3(x, y, cross)) as
+// the trace uses it (9 floats). Returns false (no BVH) when a light is
+// non-finite or ill-conditioned.
+inline bool bvh_build_lights(int n, const float (*P)[3], const float (*x)[3], const float (*y)[3],
+                             const float (*inv)[9], const float cam[3], float B, std::vector<BvhNode>& nodes,
+                             int* nodes_per_order) {
+    std::vector<BvhBox> box(n);
+    for (int i = 0; i < n; ++i) {
+        double mn = 0.0, in = 0.0, ext = 0.0, pn = 0.0;
+        const double cx = (double)x[i][1] * y[i][2] - (double)x[i][2] * y[i][1];
+        const double cy = (double)x[i][2] * y[i][0] - (double)x[i][0] * y[i][2];
+        const double cz = (double)x[i][0] * y[i][1] - (double)x[i][1] * y[i][0];
+        for (int a = 0; a < 3; ++a) {
+            mn += (double)x[i][a] * x[i][a] + (double)y[i][a] * y[i][a];
+            pn += std::fabs((double)P[i][a]);
+            ext += std::fabs((double)x[i][a]) + std::fabs((double)y[i][a]);
+        }
+        mn += cx * cx + cy * cy + cz * cz;
+        for (int k = 0; k < 9; ++k) in += (double)inv[i][k] * inv[i][k];
+        const double cond = std::sqrt(mn) * std::sqrt(in);
+        if (!std::isfinite(cond) || !std::isfinite(pn + ext) || cond > 1e4) return false;
+        float lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            const float c0 = P[i][a], c1 = P[i][a] + x[i][a], c2 = P[i][a] + y[i][a],
+                        c3 = P[i][a] + x[i][a] + y[i][a];
+            lo[a] = std::min(std::min(c0, c1), std::min(c2, c3));
+            hi[a] = std::max(std::max(c0, c1), std::max(c2, c3));
+        }
+        const double D = origin_bound(cam, B, lo, hi);
+        const double pad = 1e-5 * D + 1e-4 * (pn + ext + 1.0) + 1e-5 * cond * ext;
+        for (int a = 0; a < 3; ++a) {
+            box[i].lo[a] = (float)((double)lo[a] - pad);
+            box[i].hi[a] = (float)((double)hi[a] + pad);
+        }
+    }
+    std::vector<int> perm;
+    bvh_build_boxes(box, 2, false, 1, nodes, perm, nodes_per_order);
+    return true;
 }
 
 }  // namespace ipt

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -49,7 +51,7 @@ __device__ __forceinline__ void keep_alive(const T& v) {
 }
 constexpr int kStackFields = 6;   // pos3, res, mult, meta(i | kind<<8)
 constexpr int kPoolChunk = 256;   // work units per global atomic
-constexpr int kNumCounters = 13;
+constexpr int kNumCounters = 15;
 
 struct KParams {
     int W, H, spp, spp_offset, n_rays, depth_max;
@@ -75,6 +77,9 @@ struct KParams {
     const BvhNode* __restrict__ bvh_nodes;     // n_nodes > 0: sphere BVH (ipt_bvh.h)
     const BvhSphere* __restrict__ bvh_prims;
     int n_nodes;
+    const BvhNode* __restrict__ light_nodes;   // n_light_nodes > 0: light BVH over index ranges
+    int n_light_nodes;
+    int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
@@ -293,7 +298,8 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
     float tres = 0.0f;
     int ti = 0, tdepth = 0, tkind = 0;  // kind: 0..4 wall plane, 5 box sphere, 6+i extra sphere i
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
-             c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0, c_nodes = 0, c_tests = 0;
+             c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0, c_nodes = 0, c_tests = 0,
+             c_lnode = 0, c_ltest = 0;
 
     for (;;) {
         // -------------------------------------------------- unit refill
@@ -478,6 +484,14 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             int c = 0;
             if (LMODE == kLightsOne) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+            } else if (LMODE == kLightsGlobal && kp.cdf_bsearch) {
+                // first c with r < cdf[c] (else nl+1): the scan's answer on a
+                // non-decreasing cdf (checked at upload)
+                int hi = nl + 1;
+                while (c < hi) {
+                    const int mid = (c + hi) >> 1;
+                    if (r < LS.cdf(mid)) hi = mid; else c = mid + 1;
+                }
             } else {
                 while (c <= nl && !(r < LS.cdf(c))) ++c;
             }
@@ -588,7 +602,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             bool has_li = false;
             vec3 li_pos = v3(0, 0, 0);
             float li_pow = 0.0f;
-            for (int l = 0; l < nl; ++l) {
+            auto light_step = [&](int l) {
                 const LightDev& L = LS.light(l);
                 vec3 hp;
                 const bool h = light_trace(L, ro, rd, &hp);
@@ -597,13 +611,36 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                     const bool h2 = light_trace(L, ro, rd * (1.0f + kp.abl_zero), &hq);
                     keep_alive(light_pdf(L, ro, h2, hq));
                 }
-                if (COUNT) c_ltr += (is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u);
+                if (COUNT) ++c_ltest;
                 if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp);
                 if (h && (!has_li || length(li_pos - ro) > length(hp - ro))) {
                     has_li = true;
                     li_pos = hp;
                     li_pow = L.spow;
                 }
+            };
+            // the reference's event count: every light traced once for the
+            // pdf (iterations) and once for traceRayToLight (depth < max)
+            if (COUNT) c_ltr += (uint32_t)nl * ((is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u));
+            if (LMODE == kLightsGlobal && kp.n_light_nodes > 0) {
+                // index-ordered light BVH (ipt_bvh.h): lights met in scan order;
+                // a skipped light would add +0 to lmix and never be nearest
+                const vec3 inv = v3(safe_rcp(rd.x), safe_rcp(rd.y), safe_rcp(rd.z));
+                int i = 0;
+                while (i < kp.n_light_nodes) {
+                    const BvhNode nd = kp.light_nodes[i];
+                    if (COUNT) ++c_lnode;
+                    const bool enter = bvh_box_entry(nd, ro, inv) != inf_();
+                    if (enter && nd.leaf >= 0) {
+                        const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
+                        for (int l = first; l < first + cnt; ++l) light_step(l);
+                        i = nd.skip;
+                    } else {
+                        i = enter ? i + 1 : nd.skip;
+                    }
+                }
+            } else {
+                for (int l = 0; l < nl; ++l) light_step(l);
             }
             float mult = 0.0f;
             if (is_iter) {
@@ -694,6 +731,8 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
         atomicAdd(&kp.counters[10], (unsigned long long)c_drift);
         atomicAdd(&kp.counters[11], (unsigned long long)c_nodes);
         atomicAdd(&kp.counters[12], (unsigned long long)c_tests);
+        atomicAdd(&kp.counters[13], (unsigned long long)c_lnode);
+        atomicAdd(&kp.counters[14], (unsigned long long)c_ltest);
     }
 }
 
@@ -823,6 +862,9 @@ struct ipt_ctx {
     BvhNode* d_bvh_nodes = nullptr;
     BvhSphere* d_bvh_prims = nullptr;
     int n_nodes = 0;
+    BvhNode* d_light_nodes = nullptr;
+    int n_light_nodes = 0;
+    int cdf_bsearch = 0;
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     // work buffers
     float* d_values = nullptr;
@@ -1021,6 +1063,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.bvh_nodes = ctx->d_bvh_nodes;
         kp.bvh_prims = ctx->d_bvh_prims;
         kp.n_nodes = ctx->n_nodes;
+        kp.light_nodes = ctx->d_light_nodes;
+        kp.n_light_nodes = ctx->n_light_nodes;
+        kp.cdf_bsearch = ctx->cdf_bsearch;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
         HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
@@ -1116,7 +1161,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
 void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
+    void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters};
     for (void* b : bufs)
@@ -1163,13 +1208,48 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     std::vector<float4> sph(std::max(s->n_spheres, 1));
     for (int i = 0; i < s->n_spheres; ++i)
         sph[i] = make_float4(s->spheres[i].center[0], s->spheres[i].center[1], s->spheres[i].center[2], s->spheres[i].radius);
+    // Bound of every surface point a ray can start from: the box [-1,1]^3 and
+    // the spheres (ipt_bvh.h pads item boxes from it and the camera).
+    float B = 1.0f;
+    for (int i = 0; i < s->n_spheres; ++i)
+        B = std::max(B, std::max(std::fabs(sph[i].x), std::max(std::fabs(sph[i].y), std::fabs(sph[i].z))) +
+                            std::fabs(sph[i].w));
+    const float cam[3] = {s->camera.position[0], s->camera.position[1], s->camera.position[2]};
     std::vector<BvhNode> bnodes;
     std::vector<BvhSphere> bprims;
     int per_order = 0;
     if (s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX && s->n_spheres > 16)
-        bvh_build(reinterpret_cast<const float*>(sph.data()), s->n_spheres, bnodes, bprims, &per_order);
+        bvh_build_spheres(reinterpret_cast<const float*>(sph.data()), s->n_spheres, cam, B, bnodes, bprims,
+                          &per_order);
+    // light BVH: only for the global-memory light mode (n_lights > kLdsLights)
+    std::vector<BvhNode> lnodes;
+    int n_lnodes = 0;
+    if (nl > kLdsLights) {
+        std::vector<std::array<float, 3>> lp(nl), lx(nl), ly(nl);
+        std::vector<std::array<float, 9>> li(nl);
+        for (int i = 0; i < nl; ++i) {
+            lp[i] = {L[i].P.x, L[i].P.y, L[i].P.z};
+            lx[i] = {L[i].x.x, L[i].x.y, L[i].x.z};
+            ly[i] = {L[i].y.x, L[i].y.y, L[i].y.z};
+            for (int c = 0; c < 3; ++c) {
+                li[i][3 * c + 0] = L[i].inv.c[c].x;
+                li[i][3 * c + 1] = L[i].inv.c[c].y;
+                li[i][3 * c + 2] = L[i].inv.c[c].z;
+            }
+        }
+        if (!bvh_build_lights(nl, reinterpret_cast<const float(*)[3]>(lp.data()),
+                              reinterpret_cast<const float(*)[3]>(lx.data()),
+                              reinterpret_cast<const float(*)[3]>(ly.data()),
+                              reinterpret_cast<const float(*)[9]>(li.data()), cam, B, lnodes, &n_lnodes)) {
+            lnodes.clear();
+            n_lnodes = 0;
+        }
+    }
+    bool cdf_mono = true;
+    for (int i = 0; i <= nl; ++i)
+        if (!(cdf[i] == cdf[i]) || (i > 0 && !(cdf[i - 1] <= cdf[i]))) cdf_mono = false;
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes,
-                   ctx->d_bvh_prims};
+                   ctx->d_bvh_prims, ctx->d_light_nodes};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_lights = nullptr;
@@ -1178,6 +1258,15 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->d_bvh_nodes = nullptr;
     ctx->d_bvh_prims = nullptr;
     ctx->n_nodes = 0;
+    ctx->d_light_nodes = nullptr;
+    ctx->n_light_nodes = 0;
+    if (!lnodes.empty()) {
+        HIPCHECK(ctx, hipMalloc(&ctx->d_light_nodes, sizeof(BvhNode) * lnodes.size()));
+        HIPCHECK(ctx, hipMemcpy(ctx->d_light_nodes, lnodes.data(), sizeof(BvhNode) * lnodes.size(),
+                                hipMemcpyHostToDevice));
+        ctx->n_light_nodes = n_lnodes;
+    }
+    ctx->cdf_bsearch = cdf_mono ? 1 : 0;
     if (!bnodes.empty()) {
         HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_nodes, sizeof(BvhNode) * bnodes.size()));
         HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_prims, sizeof(BvhSphere) * bprims.size()));
@@ -1286,6 +1375,8 @@ int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
     out->drifted = h[10];
     out->bvh_nodes = h[11];
     out->sphere_tests = h[12];
+    out->light_nodes = h[13];
+    out->light_tests = h[14];
     return IPT_OK;
 }
 

@@ -43,8 +43,11 @@ def ops_from_counters(c: dict, n_spheres: int = 0) -> float:
     sphere test (§8(d): "C3 adds N x 37 per trace")."""
     kept_light = c["light_samples"] - c["skipped"]
     cosine = c["iterations"] - c["light_samples"]
+    light_bvh = c.get("light_nodes", 0) > 0
     f = (c["paths"] * OPS["camera"]
-         + c["traced_rays"] * (OPS["geom_trace"] + OPS["light_trace"])
+         + c["traced_rays"] * OPS["geom_trace"]
+         + (c["light_tests"] * OPS["light_trace"] + c["light_nodes"] * OPS["bvh_node"] if light_bvh
+            else c["traced_rays"] * OPS["light_trace"])
          + c["light_hits"] * OPS["occlusion"]
          + c["surface_hits"] * (OPS["rotate_build"] + TRANSC["rotate_build"] * TRANSC_OP_EQ)
          + c["expanded_nodes"] * OPS["mixture_weights"]
@@ -53,7 +56,8 @@ def ops_from_counters(c: dict, n_spheres: int = 0) -> float:
          + cosine * (OPS["iter_cosine"] + TRANSC["iter_cosine"] * TRANSC_OP_EQ)
          + c["skipped"] * OPS["iter_skipped"]
          + c["expanded_nodes"] * OPS["node_finalize"])
-    f += max(0, c["light_traces"] - 2 * c["traced_rays"]) * OPS["light_trace"]
+    if not light_bvh:
+        f += max(0, c["light_traces"] - 2 * c["traced_rays"]) * OPS["light_trace"]
     if "sphere_tests" in c:
         f += c["sphere_tests"] * OPS["sphere_test"] + c.get("bvh_nodes", 0) * OPS["bvh_node"]
     else:
@@ -62,8 +66,11 @@ def ops_from_counters(c: dict, n_spheres: int = 0) -> float:
 
 
 def reference_scan_ops(c: dict, n_spheres: int) -> float:
-    """Op-eq of the reference's brute-force sphere scan for the same rays."""
-    return float(c["traced_rays"]) * n_spheres * OPS["sphere_test"]
+    """Op-eq of the reference's brute-force sphere and light scans for the
+    same rays (work the BVH walks skip)."""
+    f = float(c["traced_rays"]) * n_spheres * OPS["sphere_test"]
+    f += (c["traced_rays"] + max(0, c["light_traces"] - 2 * c["traced_rays"])) * OPS["light_trace"]
+    return f
 
 
 def accumulate_bytes(n_dest_pixels: int, spp: int, with_sums: bool = True,

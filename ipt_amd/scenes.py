@@ -14,7 +14,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .capi import IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES_IN_BOX, IPT_LIGHT_AREA_DIAMOND
+from .capi import (IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES_IN_BOX, IPT_LIGHT_AREA_DIAMOND,
+                   IPT_LIGHT_AREA_TRIANGLE)
 
 f32 = np.float32
 
@@ -100,6 +101,30 @@ def splitmix64(seed):
         z = np.uint64((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9))
         z = np.uint64((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB))
         yield int(z ^ (z >> np.uint64(31)))
+
+
+def make_scene_random_lights(n: int = 64, seed: int = 7):
+    """Box + n overlapping emitters of random position, orientation and shape
+    (parallelograms via Light(corner, x, y) and triangles as addTriangleLight,
+    CollectionLighting.cpp:47-50), SplitMix64(seed). Rays cross several
+    emitters, exercising traceRayToLight's nearest rule and UnionDdf::value's
+    index-order sum over many hits."""
+    g = splitmix64(seed)
+
+    def u():
+        return f32((next(g) >> 40) * (1.0 / (1 << 24)))
+
+    lights = []
+    with np.errstate(over="ignore"):
+        for i in range(n):
+            corner = [float(f32(f32(-0.8) + f32(f32(1.4) * u()))) for _ in range(3)]
+            xs = [float(f32(f32(0.6) * u() - f32(0.3))) for _ in range(3)]
+            ys = [float(f32(f32(0.6) * u() - f32(0.3))) for _ in range(3)]
+            power = float(f32(f32(0.2) + f32(0.8) * u()))
+            lights.append({"position": corner, "x_axis": xs, "y_axis": ys, "power": power,
+                           "type": IPT_LIGHT_AREA_TRIANGLE if i % 3 == 2 else IPT_LIGHT_AREA_DIAMOND})
+    return {"geometry_kind": IPT_GEOM_SPHERE_IN_BOX, "lights": lights, "spheres": [],
+            "camera": box_camera()}
 
 
 def make_scene_spheres(n: int = 10000, seed: int = 1):

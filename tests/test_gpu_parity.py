@@ -124,6 +124,32 @@ def test_many_lights_bit_exact(gpu_ctx, oracle, k):
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
 
 
+@pytest.mark.parametrize("n", [17, 64, 300])
+def test_random_lights_bit_exact(gpu_ctx, oracle, n):
+    """Overlapping emitters of random shape/orientation above kLdsLights: the
+    index-ordered light BVH must reproduce the full scan's nearest-light rule
+    and the running UnionDdf sum with several hits per ray."""
+    desc = scenes.make_scene_random_lights(n, seed=7)
+    p = capi.make_params(20, 16, 2, n_rays=8, depth_max=6)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+def test_light_bvh_active(gpu_ctx):
+    """The 256-emitter scene runs the light BVH: far fewer light tests than
+    the reference's L traces per ray, and the reference event count intact."""
+    gpu_ctx.upload_scene(scenes.make_scene_box_lights(16))
+    p = capi.make_params(32, 32, 1, n_rays=16, depth_max=8, flags=capi.IPT_FLAG_COUNTERS)
+    img = {"pixels": np.zeros(32 * 32, np.float32), "counters": np.zeros(32 * 32, np.uint32)}
+    gpu_ctx.reset_counters()
+    gpu_ctx.render(p, img)
+    c = gpu_ctx.counters()
+    assert c["light_nodes"] > 0
+    assert c["light_tests"] < 0.1 * 256 * c["traced_rays"]
+    assert c["light_traces"] >= 256 * c["traced_rays"]
+
+
 def test_spheres_in_box_c3_scene(gpu_ctx, oracle):
     """The full 10k-sphere scene of BASELINE configs[2] (bench C3): BVH walk
     (octant orders, open-floor rays with best = inf) against the oracle's scan."""
