@@ -171,6 +171,12 @@ int ipt_shard_plan(const ipt_params* p, uint8_t* owned_rows, int32_t* cand_rows,
 
 int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out);
 int ipt_reset_counters(ipt_ctx* ctx);
+/* Phase profile of the path kernel: out[2q] = wave executions of phase q,
+ * out[2q+1] = active lanes summed over them (words 0..23, -DIPT_PROF=1
+ * builds); out[24+s] = wave-cycles in step segment s (words 24..35,
+ * -DIPT_STAMP=1 builds; scripts/prof_phases.sh). Zeros in product builds.
+ * Cleared by ipt_reset_counters. */
+int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n);
 
 /* Timing of the most recent render call's kernels (ms, HIP events on the
    launch stream): [0] = path kernel, [1] = accumulate kernel. */
@@ -181,6 +187,13 @@ int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
        5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u)      */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
+/* Device self-check of the fast math paths: for every float bit pattern b in
+ * [lo_bits, hi_bits) (hi_bits <= 2^32) compares function fn as the kernels
+ * compute it with its exact restatement, on the device. Returns the number of
+ * differing results (NaN == NaN) and the lowest differing pattern (0xffffffff
+ * if none). Used to prove a fast path exhaustively (all 2^32 inputs). */
+int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
+                       uint32_t* first_bad);
 
 #ifdef __cplusplus
 }

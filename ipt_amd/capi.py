@@ -81,8 +81,15 @@ EXPORTED_SYMBOLS = (
     "ipt_abi_version", "ipt_last_error", "ipt_create", "ipt_destroy", "ipt_upload_scene",
     "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
-    "ipt_shard_plan",
+    "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck",
 )
+
+# path-kernel phases of the IPT_PROF profile (ipt_kernels.hip IPT_PHASE ids)
+PROFILE_PHASES = ("step", "pop", "new_path", "iteration", "philox", "frame_worker",
+                  "cosine_worker", "light_sample", "trace", "geometry", "push", "wg_step")
+# step segments of the IPT_STAMP diagnostic build (IPT_STAMP_AT ids)
+STAMP_SEGMENTS = ("tail", "refill", "pop", "new_path", "post_prologue_philox", "barrier_a",
+                  "workers", "barrier_b", "direction", "lights", "geometry")
 
 _lib = None
 
@@ -116,6 +123,9 @@ def load(path: str | os.PathLike | None = None):
     lib.ipt_render_values.argtypes = [C.c_void_p, C.POINTER(Params), C.c_void_p, C.c_void_p]
     lib.ipt_get_counters.argtypes = [C.c_void_p, C.POINTER(Counters)]
     lib.ipt_reset_counters.argtypes = [C.c_void_p]
+    lib.ipt_math_selfcheck.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64,
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    lib.ipt_get_profile.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     lib.ipt_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
     lib.ipt_math_host.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
     lib.ipt_math_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
@@ -228,6 +238,24 @@ class Context:
 
     def reset_counters(self):
         _check(self.lib, self.h, self.lib.ipt_reset_counters(self.h))
+
+    def math_selfcheck(self, fn: int, lo_bits: int = 0, hi_bits: int = 1 << 32):
+        """(mismatches, first differing bit pattern) of the device fast path of
+        math fn against its exact restatement over [lo_bits, hi_bits)."""
+        bad, first = C.c_uint64(), C.c_uint32()
+        _check(self.lib, self.h, self.lib.ipt_math_selfcheck(self.h, fn, lo_bits, hi_bits, C.byref(bad),
+                                                             C.byref(first)))
+        return int(bad.value), int(first.value)
+
+    def profile(self) -> dict:
+        """{phase: (wave executions, active lanes)} from an IPT_PROF build."""
+        n = 2 * len(PROFILE_PHASES) + 12
+        buf = (C.c_uint64 * n)()
+        _check(self.lib, self.h, self.lib.ipt_get_profile(self.h, buf, n))
+        out = {ph: (int(buf[2 * i]), int(buf[2 * i + 1])) for i, ph in enumerate(PROFILE_PHASES)}
+        base = 2 * len(PROFILE_PHASES)
+        out["stamps"] = {sg: int(buf[base + i]) for i, sg in enumerate(STAMP_SEGMENTS)}
+        return out
 
     def last_kernel_ms(self):
         a, b = C.c_float(), C.c_float()

@@ -22,6 +22,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -44,6 +45,36 @@ constexpr int kBlock = 256;
 #ifndef IPT_ABL
 #define IPT_ABL 0
 #endif
+// Profiling-only builds (-DIPT_PROF=1, scripts/prof_phases.sh): per phase, the
+// number of wave executions and of active lanes in them (lane utilisation),
+// read back with ipt_get_profile().
+#ifndef IPT_PROF
+#define IPT_PROF 0
+#endif
+constexpr int kProfPhases = 12;
+#define IPT_PHASE(id)                                  \
+    if (IPT_PROF) {                                    \
+        const uint64_t pm_ = __ballot(1);              \
+        prof_w[id] += 1u;                              \
+        prof_l[id] += (uint32_t)__popcll(pm_);         \
+    }
+
+// Diagnostic stamp builds (-DIPT_STAMP=1, scripts/prof_phases.sh): wave-cycles
+// (s_memtime) spent since the previous stamp, per step segment; read their
+// SHARES (the stamps' waits forbid overlaps the real kernel has).
+#ifndef IPT_STAMP
+#define IPT_STAMP 0
+#endif
+constexpr int kStamps = 12;
+#define IPT_STAMP_AT(id)                                                                   \
+    if (IPT_STAMP) {                                                                       \
+        unsigned long long t_;                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        st_acc[id] += (uint32_t)(t_ - st_last);                                            \
+        st_last = t_;                                                                      \
+    }
 template <typename T>
 __device__ __forceinline__ void keep_alive(const T& v) {
     const float* p = reinterpret_cast<const float*>(&v);
@@ -80,6 +111,7 @@ struct KParams {
     const BvhNode* __restrict__ light_nodes;   // n_light_nodes > 0: light BVH over index ranges
     int n_light_nodes;
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
+    int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
@@ -128,10 +160,10 @@ __device__ __forceinline__ float safe_rcp(float d) {
 
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
 // r=0.5 sphere, 6+i extra sphere i (original index), -1 miss.
-template <bool COUNT>
+template <bool COUNT, int GEOM>
 __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim, uint32_t& c_nodes,
                                                 uint32_t& c_tests) {
-    if (kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
+    if (GEOM == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
     // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
     // (FractalSpheres.cpp:75-84): strict '<' in index order == minimal t,
     // lowest index among equal t, and a sphere never wins a tie with a plane.
@@ -189,11 +221,17 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
 constexpr int kLdsLights = 16;
 constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
 constexpr int kLdsCand = 512;
-constexpr int kFrameSlots = 128;  // sphere-frame builds per workgroup step (overflow retries)
-__host__ __device__ constexpr size_t scene_lds_words() {
-    return 60 + (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) + kLdsCand + 4 +
+constexpr int kFrameSlots = 64;  // sphere-frame builds per workgroup step (overflow retries)
+// LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
+// task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
+// so unsharded launches do not allocate it).
+__host__ __device__ constexpr size_t scene_lds_words(int lmode) {
+    return 60 + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) + 4 +
            12 * kFrameSlots + 3 * kBlock;
 }
+#ifndef IPT_WAVES_PER_SIMD
+#define IPT_WAVES_PER_SIMD 4
+#endif
 
 // Where the lights live during the step loop (compile time, so that no
 // generic/flat pointer is ever formed: a flat load would make the compiler
@@ -227,23 +265,25 @@ struct LightSet {
     }
 };
 
-template <int MAXSUSP, bool COUNT, int LMODE>
-__global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
+// GEOM (IPT_GEOM_*) is a template parameter so that the box instance carries
+// neither the sphere-list code nor its pointers (SGPR pressure).
+template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
+__global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const KParams kp) {
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
     float* wallf = lds + MAXSUSP * kStackFields * kBlock;     // [5][12]
     LightDev* lights_lds = reinterpret_cast<LightDev*>(wallf + 60);
     float* weights_lds = wallf + 60 + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
-    int* cand_lds = reinterpret_cast<int*>(cdf_lds + (kLdsLights + 1));
-    int* xcnt = cand_lds + kLdsCand;                          // [2 parities][frames, cosines]
+    int* xcnt = reinterpret_cast<int*>(wallf + 60 + (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
     float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [12][kFrameSlots]
     float* xcos = xfr + 12 * kFrameSlots;                      // [3][kBlock]
+    int* cand_lds = reinterpret_cast<int*>(xcos + 3 * kBlock);  // [kLdsCand] when kp.cand_lds
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     if (tid < 4) xcnt[tid] = 0;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
-    const bool cand_in_lds = sharded && kp.n_cand <= kLdsCand;
+    const bool cand_in_lds = kp.cand_lds != 0;
     if (tid < 60) wallf[tid] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
     if (LMODE == kLightsLds) {
         const float* src = reinterpret_cast<const float*>(kp.lights);
@@ -300,8 +340,18 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
              c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0, c_nodes = 0, c_tests = 0,
              c_lnode = 0, c_ltest = 0;
+    uint32_t prof_w[kProfPhases], prof_l[kProfPhases];
+    uint32_t st_acc[kStamps];
+    unsigned long long st_last = 0;
+    if (IPT_STAMP) {
+        for (int q = 0; q < kStamps; ++q) st_acc[q] = 0u;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+    }
+    if (IPT_PROF)
+        for (int q = 0; q < kProfPhases; ++q) prof_w[q] = prof_l[q] = 0u;
 
     for (;;) {
+        IPT_STAMP_AT(0);  // previous step's tail (resolve, push, stores)
         // -------------------------------------------------- unit refill
         const bool need = active && !has_path;
         const uint64_t needmask = __ballot(need);
@@ -336,11 +386,14 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             }
         }
 
+        IPT_STAMP_AT(1);  // refill
+        if (active) { IPT_PHASE(0); }
         // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
         if (active && has_path && !fresh) {
             for (;;) {
                 const int n = kp.n_rays >> tdepth;
                 if (ti < n) break;
+                IPT_PHASE(1);
                 float v = 0.0f;
                 if (isfinite_(tres))
                     v = n_pow2 ? tres * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - tdepth))
@@ -373,11 +426,13 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             }
         }
 
+        IPT_STAMP_AT(2);  // finalize + pop
         // ------------------------- phase 2: new path (render_sample body, main.cpp:192-211)
         bool have_ray = false, is_iter = false;
         vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         int rdepth = 0;
         if (active && has_path && fresh) {
+            IPT_PHASE(2);
             fresh = false;
             const unsigned long long s = unit / per_pass;
             const unsigned long long rem = unit - s * per_pass;
@@ -431,6 +486,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             }
         }
 
+        IPT_STAMP_AT(3);  // new path
         // ------------- phase 3: post the step's expensive, divergent tasks to the
         // workgroup (RotateDdf frames of sphere nodes, CosineDdf local samples) so
         // that they run on ceil(N/64) dense wave-passes instead of on every wave.
@@ -450,7 +506,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
         const bool stalled = want_frame && slot_f >= kFrameSlots;  // retry next step
         if (want_frame && !stalled) {
             vec3 nrm;
-            if (tkind == 5) {
+            if (GEOM == IPT_GEOM_SPHERE_IN_BOX || tkind == 5) {
                 nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67 (done by the worker)
             } else {
                 const float4 sp = kp.spheres[tkind - 6];
@@ -465,12 +521,14 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
         int pick = -1;
         float u1 = 0.0f, u2 = 0.0f;
         if (iter_lane) {
+            IPT_PHASE(3);
             if ((k >> 2) != blk) {
                 w.a0 = w.b0; w.a1 = w.b1; w.a2 = w.b2; w.a3 = w.b3;
                 ++blk;
                 need_b = true;
             }
             if (need_b) {
+                IPT_PHASE(4);
                 philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
                 if (IPT_ABL == 3) {
                     uint32_t q0, q1, q2, q3;
@@ -520,8 +578,11 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             xcos[0 * kBlock + slot_c] = u1;
             xcos[1 * kBlock + slot_c] = u2;
         }
+        if (IPT_PROF && wave == 0) { IPT_PHASE(11); }  // workgroup steps (one wave counts)
+        IPT_STAMP_AT(4);  // task posting, iteration prologue, Philox
         // barrier A; also the block-wide exit test (every wave runs every barrier)
         if (!__syncthreads_or(active ? 1 : 0)) break;
+        IPT_STAMP_AT(5);  // barrier A
         if (tid == 0) {
             xcnt[(1 - par) * 2 + 0] = 0;
             xcnt[(1 - par) * 2 + 1] = 0;
@@ -536,6 +597,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 if (pass < pf) {
                     const int sl = pass * 64 + lane;
                     if (sl < nf) {
+                        IPT_PHASE(5);
                         const vec3 nn = normalize(v3(xfr[0 * kFrameSlots + sl], xfr[1 * kFrameSlots + sl],
                                                      xfr[2 * kFrameSlots + sl]));
                         const Frame f = make_frame(nn);
@@ -550,6 +612,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 } else {
                     const int sl = (pc - 1 - (pass - pf)) * 64 + lane;
                     if (sl < nc) {
+                        IPT_PHASE(6);
                         const vec3 v = cosine_sample_local(xcos[0 * kBlock + sl], xcos[1 * kBlock + sl]);
                         if (IPT_ABL == 2)
                             keep_alive(cosine_sample_local(xcos[0 * kBlock + sl] + kp.abl_zero, xcos[1 * kBlock + sl]));
@@ -560,7 +623,9 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 }
             }
         }
+        IPT_STAMP_AT(6);  // worker passes (frames, cosine samples)
         __syncthreads();  // barrier B: results visible
+        IPT_STAMP_AT(7);  // barrier B
         if (want_frame && !stalled) {
             tfr.m0 = v3(xfr[0 * kFrameSlots + slot_f], xfr[1 * kFrameSlots + slot_f], xfr[2 * kFrameSlots + slot_f]);
             tfr.m1 = v3(xfr[3 * kFrameSlots + slot_f], xfr[4 * kFrameSlots + slot_f], xfr[5 * kFrameSlots + slot_f]);
@@ -573,6 +638,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
         if (iter_lane) {
             vec3 dir = v3(0, 0, 0);
             if (pick < nl) {
+                IPT_PHASE(7);
                 dir = light_sample_dir(LS.light(pick), tpos, u1, u2);
                 if (IPT_ABL == 7) keep_alive(light_sample_dir(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
                 if (COUNT) ++c_lsamp;
@@ -593,9 +659,10 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             }
         }
         ++step;
-
+        IPT_STAMP_AT(8);  // direction
         // --------------------------------------------- phase 4: trace + resolve
         if (have_ray) {
+            IPT_PHASE(8);
             // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
             // and the child's CollectionLighting::traceRayToLight
             float lmix = 0.0f;
@@ -642,6 +709,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             } else {
                 for (int l = 0; l < nl; ++l) light_step(l);
             }
+            IPT_STAMP_AT(9);  // light traces + pdf
             float mult = 0.0f;
             if (is_iter) {
                 const float sdf_val = frame_cosine_value(tfr, rd);
@@ -654,12 +722,14 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
             vec3 si_pos = v3(0, 0, 0);
             int prim = -1;
             if (rdepth < kp.depth_max) {
-                const float t = trace_geometry<COUNT>(kp, ro, rd, &prim, c_nodes, c_tests);
+                IPT_PHASE(9);
+                const float t = trace_geometry<COUNT, GEOM>(kp, ro, rd, &prim, c_nodes, c_tests);
                 if (IPT_ABL == 5) {
                     int p2;
-                    keep_alive(trace_geometry<false>(kp, ro, rd * (1.0f + kp.abl_zero), &p2, c_nodes, c_tests));
+                    keep_alive(trace_geometry<false, GEOM>(kp, ro, rd * (1.0f + kp.abl_zero), &p2, c_nodes, c_tests));
                     keep_alive(p2);
                 }
+                IPT_STAMP_AT(10);  // mixture value + geometry trace
                 const bool has_si = prim >= 0;
                 if (COUNT) {
                     ++c_traced;
@@ -683,6 +753,7 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
                 }
             }
             if (push) {
+                IPT_PHASE(10);
                 if (is_iter) {
                     float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
                     b[0 * kBlock] = tpos.x;
@@ -717,6 +788,14 @@ __global__ __launch_bounds__(kBlock, 4) void path_kernel(const KParams kp) {
         }
     }
 
+    if (IPT_STAMP && lane == 0)
+        for (int q = 0; q < kStamps; ++q)
+            atomicAdd(&kp.counters[kNumCounters + 2 * kProfPhases + q], (unsigned long long)st_acc[q]);
+    if (IPT_PROF && lane == 0)
+        for (int q = 0; q < kProfPhases; ++q) {
+            atomicAdd(&kp.counters[kNumCounters + 2 * q], (unsigned long long)prof_w[q]);
+            atomicAdd(&kp.counters[kNumCounters + 2 * q + 1], (unsigned long long)prof_l[q]);
+        }
     if (COUNT) {
         atomicAdd(&kp.counters[0], (unsigned long long)c_paths);
         atomicAdd(&kp.counters[1], (unsigned long long)c_traced);
@@ -839,6 +918,26 @@ __global__ void math_kernel(int fn, const float* in, float* out, long long n) {
     if (i < n) out[i] = math_fn(fn, in[i]);
 }
 
+// Exact restatement of math_fn (differs only where the device uses a fast
+// path, i.e. fn 3): the reference for ipt_math_selfcheck.
+__device__ float math_fn_exact(int fn, float x) { return fn == 3 ? acos_f64_to_f32_exact(x) : math_fn(fn, x); }
+
+__global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long long n,
+                                 unsigned long long* bad, unsigned int* first) {
+    unsigned long long local = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t b = (uint32_t)(lo + i);
+        const float x = u2f(b);
+        const float a = math_fn(fn, x), e = math_fn_exact(fn, x);
+        if (!(f2u(a) == f2u(e) || (a != a && e != e))) {
+            ++local;
+            atomicMin(first, b);
+        }
+    }
+    if (local) atomicAdd(bad, local);
+}
+
 // ---------------------------------------------------------------- context
 std::mutex g_err_mu;
 std::string g_err_global;
@@ -865,6 +964,7 @@ struct ipt_ctx {
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
+    int bpc_override = 0;
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     // work buffers
     float* d_values = nullptr;
@@ -979,22 +1079,29 @@ int needed_susp(const ipt_params* p) {
     return maxpush < 0 ? 0 : maxpush;  // suspended levels = depth of deepest pushed node
 }
 
-template <int MAXSUSP, bool COUNT, int LMODE>
-int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
-    const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words()) * sizeof(float);
-    HIPCHECK(ctx, hipFuncSetAttribute((const void*)path_kernel<MAXSUSP, COUNT, LMODE>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
+int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
+    const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE) +
+                        (kp.cand_lds ? kLdsCand : 0)) * sizeof(float);
+    const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
+    HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // persistent grid: every block the CUs can hold at once (a work queue, no
     // inter-block waits, so an over-reported residency only queues blocks)
     int bpc = 0;
-    HIPCHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                      &bpc, (const void*)path_kernel<MAXSUSP, COUNT, LMODE>, kBlock, lds));
+    HIPCHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds));
     bpc = std::max(1, std::min(bpc, 8));
+    if (ctx->bpc_override > 0) bpc = std::min(bpc, ctx->bpc_override);  // IPT_BLOCKS_PER_CU (profiling)
     ctx->blocks_per_cu = bpc;
     dim3 grid(ctx->n_cu * bpc), block(kBlock);
-    hipLaunchKernelGGL((path_kernel<MAXSUSP, COUNT, LMODE>), grid, block, lds, st, kp);
+    hipLaunchKernelGGL((path_kernel<MAXSUSP, COUNT, LMODE, GEOM>), grid, block, lds, st, kp);
     HIPCHECK(ctx, hipGetLastError());
     return IPT_OK;
+}
+template <int MAXSUSP, bool COUNT, int LMODE>
+int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
+    if (kp.geometry_kind == IPT_GEOM_SPHERES_IN_BOX)
+        return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES_IN_BOX>(ctx, kp, st);
+    return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
 }
 template <int MAXSUSP, bool COUNT>
 int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
@@ -1066,6 +1173,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.light_nodes = ctx->d_light_nodes;
         kp.n_light_nodes = ctx->n_light_nodes;
         kp.cdf_bsearch = ctx->cdf_bsearch;
+        kp.cand_lds = (p->n_shards > 1 && p->tile_rows > 0 && kp.n_cand <= kLdsCand) ? 1 : 0;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
         HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
@@ -1142,18 +1250,19 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     ipt_ctx* ctx = new ipt_ctx();
     ctx->device = hip_device;
     ctx->n_cu = prop.multiProcessorCount;
+    if (const char* e = std::getenv("IPT_BLOCKS_PER_CU")) ctx->bpc_override = std::atoi(e);  // profiling only
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return fail(nullptr, IPT_E_DEVICE, "stream creation failed");
     }
     for (auto& e : ctx->ev) hipEventCreate(&e);
     if (hipMalloc(&ctx->d_unit, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * kNumCounters) != hipSuccess ||
+        hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps)) != hipSuccess ||
         hipMalloc(&ctx->d_wall, sizeof(Frame) * 5) != hipSuccess) {
         ipt_destroy(ctx);
         return fail(nullptr, IPT_E_OOM, "hipMalloc failed");
     }
-    hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * kNumCounters);
+    hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps));
     *out = ctx;
     return IPT_OK;
 }
@@ -1380,10 +1489,19 @@ int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
     return IPT_OK;
 }
 
+int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n) {
+    if (!ctx || !out || n < 0) return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    unsigned long long h[2 * kProfPhases + kStamps];
+    HIPCHECK(ctx, hipMemcpy(h, ctx->d_counters + kNumCounters, sizeof h, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n && i < 2 * kProfPhases + kStamps; ++i) out[i] = h[i];
+    return IPT_OK;
+}
+
 int ipt_reset_counters(ipt_ctx* ctx) {
     if (!ctx) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
-    HIPCHECK(ctx, hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * kNumCounters));
+    HIPCHECK(ctx, hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps)));
     return IPT_OK;
 }
 
@@ -1420,6 +1538,34 @@ int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n
     HIPCHECK(ctx, hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost));
     hipFree(din);
     hipFree(dout);
+    return IPT_OK;
+}
+
+int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
+                       uint32_t* first_bad) {
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 8 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+        return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    unsigned long long* d_bad = nullptr;
+    unsigned int* d_first = nullptr;
+    HIPCHECK(ctx, hipMalloc(&d_bad, sizeof(unsigned long long)));
+    HIPCHECK(ctx, hipMalloc(&d_first, sizeof(unsigned int)));
+    HIPCHECK(ctx, hipMemsetAsync(d_bad, 0, sizeof(unsigned long long), ctx->stream));
+    HIPCHECK(ctx, hipMemsetAsync(d_first, 0xff, sizeof(unsigned int), ctx->stream));
+    const unsigned long long n = hi_bits - lo_bits;
+    if (n > 0)
+        hipLaunchKernelGGL(selfcheck_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, ctx->stream, fn,
+                           (unsigned long long)lo_bits, n, d_bad, d_first);
+    HIPCHECK(ctx, hipGetLastError());
+    unsigned long long hb = 0;
+    unsigned int hf = 0;
+    HIPCHECK(ctx, hipMemcpyAsync(&hb, d_bad, sizeof hb, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipMemcpyAsync(&hf, d_first, sizeof hf, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    hipFree(d_bad);
+    hipFree(d_first);
+    *mismatches = hb;
+    *first_bad = hf;
     return IPT_OK;
 }
 

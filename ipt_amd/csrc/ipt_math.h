@@ -340,7 +340,63 @@ IPT_HD double acos_d_(double x) {
     }
     return res;
 }
-IPT_HD float acos_f64_to_f32(float x) { return (float)acos_d_((double)x); }
+IPT_HD float acos_f64_to_f32_exact(float x) { return (float)acos_d_((double)x); }
+
+// RotateDdf's angle (float)acos((double)x) (ddf_detail.h:82), fast device path.
+// acos_d_ costs two IEEE f64 divisions and an IEEE f64 sqrt, each a long
+// correction sequence on gfx950. Here fdlibm's formulas are evaluated with the
+// hardware f64 reciprocal / reciprocal-sqrt refined by Newton steps (relative
+// error of A a few 1e-16), and the float rounding of A is accepted when A(1-d)
+// and A(1+d), d = 2^-44, round to the same float: rounding is monotonic, so
+// the exact value and fdlibm's (both within d of A) round there too (Ziv's
+// test). Otherwise, and for |x| >= 1, the exact restatement decides. Equal to
+// acos_f64_to_f32_exact on every float (device self-check over all 2^32
+// inputs, tests/test_gpu_parity.py::test_fast_acos_exhaustive).
+IPT_HD float acos_f64_to_f32(float xf) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double x = (double)xf;
+    const double ax = __builtin_fabs(x);
+    const double pi = u2d(0x400921fb54442d18ull);
+    const double pio2_hi = u2d(0x3ff921fb54442d18ull);
+    const double pio2_lo = u2d(0x3c91a62633145c07ull);
+    const double pS0 = u2d(0x3fc5555555555555ull), pS1 = u2d(0xbfd4d61203eb6f7dull),
+                 pS2 = u2d(0x3fc9c1550e884455ull), pS3 = u2d(0xbfa48228b5688f3bull),
+                 pS4 = u2d(0x3f49efe07501b288ull), pS5 = u2d(0x3f023de10dfdf709ull);
+    const double qS1 = u2d(0xc0033a271c8a2d4bull), qS2 = u2d(0x40002ae59c598ac8ull),
+                 qS3 = u2d(0xbfe6066c1b8d0159ull), qS4 = u2d(0x3fb3b8c5b12e9282ull);
+    const bool small = ax < 0.5;
+    const double z = small ? x * x : (1.0 - ax) * 0.5;
+    const double p = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                         __builtin_fma(z, pS5, pS4), pS3), pS2), pS1), pS0);
+    const double q = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, qS4, qS3), qS2), qS1), 1.0);
+    double y = __builtin_amdgcn_rcp(q);
+    y = __builtin_fma(y, __builtin_fma(-q, y, 1.0), y);
+    y = __builtin_fma(y, __builtin_fma(-q, y, 1.0), y);
+    const double r = p * y;
+    // sqrt(z) by Goldschmidt from rsq (z in (0, 0.25] off the small branch)
+    const double zs = small ? 0.25 : z;
+    const double g0 = __builtin_amdgcn_rsq(zs);
+    double sg = zs * g0, h = 0.5 * g0;
+    double t = __builtin_fma(-sg, h, 0.5);
+    sg = __builtin_fma(sg, t, sg);
+    h = __builtin_fma(h, t, h);
+    t = __builtin_fma(-sg, sg, zs);
+    sg = __builtin_fma(t, h, sg);
+    double A;
+    if (small)
+        A = pio2_hi - (x - (pio2_lo - x * r));
+    else if (x < 0.0)
+        A = pi - 2.0 * (sg + (r * sg - pio2_lo));
+    else
+        A = 2.0 * (sg + r * sg);
+    const double d = u2d(0x3d30000000000000ull);  // 2^-44
+    const float lo = (float)(A * (1.0 - d)), hi = (float)(A * (1.0 + d));
+    if (lo == hi && ax < 1.0) return lo;
+    return (float)acos_d_(x);
+#else
+    return acos_f64_to_f32_exact(xf);
+#endif
+}
 
 // --------------------------------------------------- mixed-precision helpers
 // The reference compares floats against the double literal 1e-6

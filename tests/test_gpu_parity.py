@@ -84,6 +84,14 @@ def test_device_math_matches_host(gpu_ctx, fn):
         assert same.all(), (fn, x[~same][:4], d[~same][:4], h[~same][:4])
 
 
+def test_fast_acos_exhaustive(gpu_ctx):
+    """The device's fast (float)acos((double)x) (Ziv test + exact fallback,
+    ipt_math.h) equals the exact restatement on all 2^32 float inputs, which
+    equals glibc on every float (test_math_exhaustive.py)."""
+    bad, first = gpu_ctx.math_selfcheck(capi.MATH_FNS["acos_f64_f32"])
+    assert bad == 0, (bad, hex(first))
+
+
 @pytest.mark.parametrize("n_shards", [2, 3])
 def test_sharded_render_matches_whole_frame(gpu_ctx, oracle, n_shards):
     """Tile-sharded rendering (one shard per call, as one rank per GPU does)
