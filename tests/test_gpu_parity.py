@@ -84,6 +84,30 @@ def test_device_math_matches_host(gpu_ctx, fn):
         assert same.all(), (fn, x[~same][:4], d[~same][:4], h[~same][:4])
 
 
+def test_cli_render_matches_oracle(gpu_ctx, oracle, tmp_path):
+    """The C++ host path end to end: ipt_render (ipt_amd/host/, scene built by
+    the C++ sample scenes, two progressive batches) writes the same
+    GridRenderPlane pixels and counters as the oracle's accumulate."""
+    import subprocess
+    import __graft_entry__ as ge
+    ge.build_host()
+    W, H, spp, passes = 48, 40, 2, 2
+    r = subprocess.run([str(ge.HOST_BIN), "--scene", "box", "--width", str(W), "--height", str(H),
+                        "--spp", str(spp), "--passes", str(passes), "--out", str(tmp_path / "r.png"),
+                        "--pfm", str(tmp_path / "r.pfm"), "--counts", str(tmp_path / "r.u32")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    raw = (tmp_path / "r.pfm").read_bytes()
+    hdr_end = raw.index(b"-1.0\n") + 5
+    px = np.frombuffer(raw[hdr_end:], np.float32).reshape(H, W)[::-1].reshape(-1)
+    cnt = np.fromfile(tmp_path / "r.u32", np.uint32)
+    ov, oc = ob.render_values(scenes.make_scene_box(), capi.make_params(W, H, spp * passes))
+    ref = ob.accumulate(ov, oc)
+    assert np.array_equal(cnt, ref["counters"])
+    assert np.array_equal(_bits(px), _bits(ref["pixels"]))
+    assert (tmp_path / "r.png").read_bytes()[:4] == b"\x89PNG"
+
+
 def test_fast_acos_exhaustive(gpu_ctx):
     """The device's fast (float)acos((double)x) (Ziv test + exact fallback,
     ipt_math.h) equals the exact restatement on all 2^32 float inputs, which
