@@ -258,8 +258,10 @@ def main():
             "bvh_nodes_per_trace": (cnt["bvh_nodes"] / max(cnt["traced_rays"], 1)) if desc.get("spheres") else None,
             "sphere_tests_per_trace": (cnt["sphere_tests"] / max(cnt["traced_rays"], 1)) if desc.get("spheres") else None,
             "light_tests_per_trace": cnt["light_tests"] / max(cnt["traced_rays"], 1),
+            # the reference's full sphere/light scans, only where a BVH replaced them
             "reference_scan_ops_per_path": (roofline.reference_scan_ops(cnt, len(desc.get("spheres", [])))
-                                            / cnt["paths"]),
+                                            / cnt["paths"]
+                                            if cnt["bvh_nodes"] or cnt["light_nodes"] else None),
             "launch_ms": launch_s * 1e3,
             "note": ("algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
                      "counters) per launch / HIP-event launch time; VALU issue peak "

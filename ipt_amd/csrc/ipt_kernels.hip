@@ -221,13 +221,16 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
 constexpr int kLdsLights = 16;
 constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
 constexpr int kLdsCand = 512;
-constexpr int kFrameSlots = 64;  // sphere-frame builds per workgroup step (overflow retries)
+// sphere-frame builds per workgroup step (overflow lanes retry next step):
+// the box scene makes ~25 per step, the sphere-list scene (nearly every hit a
+// sphere) well over 64
+__host__ __device__ constexpr int frame_slots(int geom) { return geom == IPT_GEOM_SPHERES_IN_BOX ? 256 : 64; }
 // LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
 // task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
 // so unsharded launches do not allocate it).
-__host__ __device__ constexpr size_t scene_lds_words(int lmode) {
+__host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
     return 60 + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) + 4 +
-           12 * kFrameSlots + 3 * kBlock;
+           12 * (size_t)frame_slots(geom) + 3 * kBlock;
 }
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4
@@ -269,6 +272,7 @@ struct LightSet {
 // neither the sphere-list code nor its pointers (SGPR pressure).
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const KParams kp) {
+    constexpr int kFrameSlots = frame_slots(GEOM);
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
     float* wallf = lds + MAXSUSP * kStackFields * kBlock;     // [5][12]
@@ -1081,7 +1085,7 @@ int needed_susp(const ipt_params* p) {
 
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
-    const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE) +
+    const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
                         (kp.cand_lds ? kLdsCand : 0)) * sizeof(float);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
