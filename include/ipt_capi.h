@@ -184,7 +184,9 @@ int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
 
 /* ---- portable-math probes (same code as the kernels), for tests ---------
    fn: 0 acosf, 1 sinf, 2 cosf, 3 (float)acos((double)x), 4 sincosf->sin,
-       5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u)      */
+       5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u),
+       9 a/b over the division pairs of the fast-division proof (x's bit
+         pattern -> an in-range numerator and hashed denominator)            */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
 /* Device self-check of the fast math paths: for every float bit pattern b in

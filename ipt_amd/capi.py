@@ -280,7 +280,7 @@ def math_host(fn: int, x: np.ndarray) -> np.ndarray:
 
 
 MATH_FNS = {"acosf": 0, "sinf": 1, "cosf": 2, "acos_f64_f32": 3, "sincosf_sin": 4,
-            "sincosf_cos": 5, "sqrtf": 6, "div_pi": 7, "two_pi_times": 8}
+            "sincosf_cos": 5, "sqrtf": 6, "div_pi": 7, "two_pi_times": 8, "div_pairs": 9}
 
 
 def shard_plan(p: Params):

@@ -37,7 +37,10 @@ using namespace ipt;
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef IPT_BLOCK
+#define IPT_BLOCK 256
+#endif
+constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOCK for experiments)
 
 // Profiling-only builds (-DIPT_ABL=n, scripts/ablate.sh): phase n is computed a
 // second time on a perturbed input and kept alive, so the wall-time delta is
@@ -718,7 +721,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             if (is_iter) {
                 const float sdf_val = frame_cosine_value(tfr, rd);
                 const float mix = lmix + w_sdf * sdf_val;
-                mult = sdf_val / mix;
+                mult = div_(sdf_val, mix);
             }
             // child ray_power (main.cpp:100-143)
             float cv = 0.0f;
@@ -903,6 +906,23 @@ __global__ __launch_bounds__(256) void accumulate_kernel(AParams ap) {
 }
 
 // ----------------------------------------------------------- math probes
+// Division pairs for the fast-division proof (fn 9): every 32-bit pattern b
+// maps to a numerator with b's sign and mantissa and a biased exponent in
+// [87, 167] (or +-0 when b's exponent field is 0) and a hashed denominator in
+// the same range, so every wave of the self-check takes div_'s fast path.
+__device__ __host__ inline float div_pair_a(uint32_t b) {
+    const uint32_t e = (b >> 23) & 0xffu;
+    if (e == 0u) return u2f(b & 0x80000000u);
+    return u2f((b & 0x807fffffu) | ((87u + e % 81u) << 23));
+}
+__device__ __host__ inline float div_pair_b(uint32_t b) {
+    uint32_t h = b * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    return u2f((h & 0x807fffffu) | ((87u + ((h >> 23) & 0xffu) % 81u) << 23));
+}
+
 __device__ __host__ inline float math_fn(int fn, float x) {
     switch (fn) {
         case 0: return acosf_(x);
@@ -914,6 +934,7 @@ __device__ __host__ inline float math_fn(int fn, float x) {
         case 6: return sqrt_(x);
         case 7: return div_pi_to_f32(x);
         case 8: return two_pi_times(x);
+        case 9: return div_(div_pair_a(f2u(x)), div_pair_b(f2u(x)));
         default: return 0.0f;
     }
 }
@@ -924,7 +945,12 @@ __global__ void math_kernel(int fn, const float* in, float* out, long long n) {
 
 // Exact restatement of math_fn (differs only where the device uses a fast
 // path, i.e. fn 3): the reference for ipt_math_selfcheck.
-__device__ float math_fn_exact(int fn, float x) { return fn == 3 ? acos_f64_to_f32_exact(x) : math_fn(fn, x); }
+__device__ float math_fn_exact(int fn, float x) {
+    if (fn == 3) return acos_f64_to_f32_exact(x);
+    if (fn == 6) return __builtin_sqrtf(x);                                      // IEEE (compiler sequence)
+    if (fn == 9) return div_pair_a(f2u(x)) / div_pair_b(f2u(x));                // IEEE (compiler sequence)
+    return math_fn(fn, x);
+}
 
 __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long long n,
                                  unsigned long long* bad, unsigned int* first) {
@@ -1517,7 +1543,7 @@ int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms) {
 }
 
 int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
-    if (!in || !out || n < 0 || fn < 0 || fn > 8) return IPT_E_INVALID;
+    if (!in || !out || n < 0 || fn < 0 || fn > 9) return IPT_E_INVALID;
     const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
@@ -1529,7 +1555,7 @@ int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
 }
 
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n) {
-    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 8) return IPT_E_INVALID;
+    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 9) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     float *din = nullptr, *dout = nullptr;
     HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * 4));
@@ -1547,7 +1573,7 @@ int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
                        uint32_t* first_bad) {
-    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 8 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 9 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
         return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     unsigned long long* d_bad = nullptr;

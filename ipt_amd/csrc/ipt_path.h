@@ -101,7 +101,7 @@ IPT_HD vec3 cosine_sample_local(float u1, float u2) {
 IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
     const float dp = sgn * da;
     if (lt_1em6(fabs_(dp))) return inf_();
-    const float t = (1.0f - sgn * oa) / dp;
+    const float t = div_(1.0f - sgn * oa, dp);
     const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
     if (fabs_(px) > 1.0f || fabs_(py) > 1.0f || fabs_(pz) > 1.0f) return inf_();
     if (dp < 0.0f) return inf_();
@@ -179,7 +179,7 @@ IPT_HD bool gt_1em6(float f) { return f > u2f(0x358637bdu); }
 IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit) {
     const float n_dir = dot(L.n, d);
     if (lt_1em6(fabs_(n_dir)) || n_dir > 0.0f) return false;
-    const float t = dot(L.n, L.P - o) / n_dir;
+    const float t = div_(dot(L.n, L.P - o), n_dir);
     if (lt_1em6(t)) return false;
     const vec3 rel = (o + d * t) - L.P;
     const vec3 coord = mul(L.inv, rel);
@@ -202,7 +202,7 @@ IPT_HD float light_pdf(const LightDev& L, vec3 o, bool has, vec3 hit) {
     if (cosinus < 0.0f) return 0.0f;
     const vec3 ho = hit - o;
     const float decay = dot(ho, ho);
-    return decay / cosinus / L.area;
+    return div_(div_(decay, cosinus), L.area);
 }
 
 // DdfFromLight::sample via AreaLight::sample (lighting.cpp:125-134, 93-104).

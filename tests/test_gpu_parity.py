@@ -108,12 +108,15 @@ def test_cli_render_matches_oracle(gpu_ctx, oracle, tmp_path):
     assert (tmp_path / "r.png").read_bytes()[:4] == b"\x89PNG"
 
 
-def test_fast_acos_exhaustive(gpu_ctx):
-    """The device's fast (float)acos((double)x) (Ziv test + exact fallback,
-    ipt_math.h) equals the exact restatement on all 2^32 float inputs, which
-    equals glibc on every float (test_math_exhaustive.py)."""
-    bad, first = gpu_ctx.math_selfcheck(capi.MATH_FNS["acos_f64_f32"])
-    assert bad == 0, (bad, hex(first))
+@pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs"])
+def test_fast_math_exhaustive(gpu_ctx, fn):
+    """The device fast paths equal their exact references on all 2^32 inputs:
+    (float)acos((double)x) (Ziv test + exact fallback) vs the fdlibm
+    restatement (== glibc on every float, test_math_exhaustive.py); sqrtf and
+    a/b (range-guarded correction cores, ipt_math.h) vs the compiler's IEEE
+    sequences (division over 2^32 in-range / zero-numerator pairs)."""
+    bad, first = gpu_ctx.math_selfcheck(capi.MATH_FNS[fn])
+    assert bad == 0, (fn, bad, hex(first))
 
 
 @pytest.mark.parametrize("n_shards", [2, 3])
