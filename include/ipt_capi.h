@@ -182,6 +182,18 @@ int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n);
    launch stream): [0] = path kernel, [1] = accumulate kernel. */
 int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
 
+/* ---- image post-process on the GPU, bit-exact --------
+   ipt_smooth: GridRenderPlane::smooth(side) (in_place = 1: pixels are
+   replaced, as the reference's in-place filter leaves them) or
+   computeSmoothedMax(side) (in_place = 0: pixels untouched); *max_value gets
+   the reference's max_value (GridRenderPlane.cpp:10-59). Host buffers
+   (width*height floats, row-major). side 1 is undefined behaviour in the
+   reference (its size_t loop runs past row 0): IPT_E_UNSUPPORTED.
+   ipt_glare: Gui's glare bloom (gui.cpp:28-52), out = glare(in, cutoff);
+   images up to 4096 x 4096. */
+int ipt_smooth(ipt_ctx* ctx, float* pixels, int width, int height, int side, int in_place, float* max_value);
+int ipt_glare(ipt_ctx* ctx, const float* in, float* out, int width, int height, float cutoff);
+
 /* ---- portable-math probes (same code as the kernels), for tests ---------
    fn: 0 acosf, 1 sinf, 2 cosf, 3 (float)acos((double)x), 4 sincosf->sin,
        5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u),

@@ -81,7 +81,7 @@ EXPORTED_SYMBOLS = (
     "ipt_abi_version", "ipt_last_error", "ipt_create", "ipt_destroy", "ipt_upload_scene",
     "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
-    "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck",
+    "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck", "ipt_smooth", "ipt_glare",
 )
 
 # path-kernel phases of the IPT_PROF profile (ipt_kernels.hip IPT_PHASE ids)
@@ -125,6 +125,9 @@ def load(path: str | os.PathLike | None = None):
     lib.ipt_reset_counters.argtypes = [C.c_void_p]
     lib.ipt_math_selfcheck.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64,
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    lib.ipt_smooth.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                               C.POINTER(C.c_float)]
+    lib.ipt_glare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float]
     lib.ipt_get_profile.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     lib.ipt_last_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
     lib.ipt_math_host.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
@@ -246,6 +249,23 @@ class Context:
         _check(self.lib, self.h, self.lib.ipt_math_selfcheck(self.h, fn, lo_bits, hi_bits, C.byref(bad),
                                                              C.byref(first)))
         return int(bad.value), int(first.value)
+
+    def smooth(self, pixels: np.ndarray, width: int, height: int, side: int, in_place: bool = True):
+        """GridRenderPlane::smooth (in_place) / computeSmoothedMax on the GPU:
+        returns (pixels after the call, max_value)."""
+        px = np.ascontiguousarray(pixels, dtype=np.float32).copy()
+        mx = C.c_float()
+        _check(self.lib, self.h, self.lib.ipt_smooth(self.h, px.ctypes.data, width, height, side,
+                                                     1 if in_place else 0, C.byref(mx)))
+        return px, float(mx.value)
+
+    def glare(self, img: np.ndarray, width: int, height: int, cutoff: float) -> np.ndarray:
+        """Gui's glare bloom (gui.cpp:28-52) on the GPU."""
+        src = np.ascontiguousarray(img, dtype=np.float32)
+        out = np.empty_like(src)
+        _check(self.lib, self.h, self.lib.ipt_glare(self.h, src.ctypes.data, out.ctypes.data, width, height,
+                                                    C.c_float(cutoff)))
+        return out
 
     def profile(self) -> dict:
         """{phase: (wave executions, active lanes)} from an IPT_PROF build."""

@@ -31,6 +31,7 @@
 
 #include "../../include/ipt_capi.h"
 #include "ipt_bvh.h"
+#include "ipt_internal.h"
 #include "ipt_path.h"
 
 using namespace ipt;
@@ -1254,6 +1255,14 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
 }
 
 }  // namespace
+
+// Hooks for the library's other translation units (ipt_internal.h).
+namespace ipt_internal {
+int ctx_fail(ipt_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
+hipStream_t ctx_stream(ipt_ctx* ctx) { return ctx->stream; }
+int ctx_device(ipt_ctx* ctx) { return ctx->device; }
+int ctx_cus(ipt_ctx* ctx) { return ctx->n_cu; }
+}  // namespace ipt_internal
 
 extern "C" {
 

@@ -265,6 +265,24 @@ void GpuRenderer::last_kernel_ms(float* path_ms, float* accumulate_ms) const {
     check(ctx_, ipt_last_kernel_ms(ctx_, path_ms, accumulate_ms));
 }
 
+void GpuRenderer::smooth(GridRenderPlane& plane, size_t side) {
+    float mx = 0.0f;
+    check(ctx_, ipt_smooth(ctx_, plane.pixels.data(), (int)plane.width, (int)plane.height, (int)side, 1, &mx));
+    plane.max_value = mx;
+}
+
+void GpuRenderer::computeSmoothedMax(GridRenderPlane& plane, size_t side) {
+    float mx = 0.0f;
+    check(ctx_, ipt_smooth(ctx_, plane.pixels.data(), (int)plane.width, (int)plane.height, (int)side, 0, &mx));
+    plane.max_value = mx;
+}
+
+std::vector<float> GpuRenderer::glare(const GridRenderPlane& plane, float cutoff) {
+    std::vector<float> out(plane.pixels.size());
+    check(ctx_, ipt_glare(ctx_, plane.pixels.data(), out.data(), (int)plane.width, (int)plane.height, cutoff));
+    return out;
+}
+
 void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, const RenderParams& p, int device) {
     GpuRenderer r(device);
     r.upload(scene);
@@ -380,6 +398,30 @@ void write_png_gray8(const std::string& path, size_t w, size_t hgt, const std::v
     chunk(f, "IDAT", z);
     chunk(f, "IEND", {});
     if (!f) throw IptError(IPT_E_INVALID, "write failed: " + path);
+}
+
+int n_val(float val, float max, float contrast, float gamma) {
+    float adj = val * contrast / max;
+    adj = std::min(adj, contrast);
+    adj = std::max(adj, 1.0f);
+    float fn = std::log(adj) / std::log(contrast);  // float overloads, as main.cpp's `using namespace std`
+    fn = std::pow(fn, gamma);
+    int n = 256 * fn;
+    n = std::max(0, n);
+    n = std::min(255, n);
+    return n;
+}
+
+void write_pgm(const std::string& path, const GridRenderPlane& plane, float contrast, float gamma) {
+    FILE* fp = std::fopen(path.c_str(), "wb");
+    if (!fp) throw IptError(IPT_E_INVALID, "cannot open " + path);
+    std::fprintf(fp, "P2\n%lu %lu\n%d\n", (unsigned long)plane.width, (unsigned long)plane.height, 255);
+    for (size_t y = 0; y < plane.height; ++y) {
+        for (size_t x = 0; x < plane.width; ++x)
+            std::fprintf(fp, "%d ", n_val(plane.pixels[y * plane.width + x], plane.max_value, contrast, gamma));
+        std::fprintf(fp, "\n");
+    }
+    std::fclose(fp);
 }
 
 void write_pfm(const std::string& path, const GridRenderPlane& plane) {

@@ -158,6 +158,11 @@ class GpuRenderer {
     void render(GridRenderPlane& plane, const RenderParams& p);
     ipt_counters counters() const;
     void last_kernel_ms(float* path_ms, float* accumulate_ms) const;
+    // GridRenderPlane::smooth / computeSmoothedMax (GridRenderPlane.cpp:10-59) on the GPU
+    void smooth(GridRenderPlane& plane, size_t side);
+    void computeSmoothedMax(GridRenderPlane& plane, size_t side);
+    // Gui's glare bloom (gui.cpp:28-52) of the plane's pixels
+    std::vector<float> glare(const GridRenderPlane& plane, float cutoff);
     ipt_ctx* handle() const { return ctx_; }
 
    private:
@@ -178,5 +183,9 @@ void write_png_gray8(const std::string& path, size_t width, size_t height, const
 // Raw outputs: PFM (float pixels, bottom-to-top rows per the format) and a
 // little binary dump of counters.
 void write_pfm(const std::string& path, const GridRenderPlane& plane);
+// main.cpp's PGM writer (main.cpp:225-235 n_val, 297-309): ASCII P2, each pixel
+// mapped by log(clamp(v*contrast/max, 1, contrast))/log(contrast), ^gamma, *256.
+int n_val(float val, float max, float contrast, float gamma);
+void write_pgm(const std::string& path, const GridRenderPlane& plane, float contrast = 500.0f, float gamma = 0.6f);
 
 }  // namespace ipt

@@ -9,6 +9,11 @@
 //              [--width 640] [--height 640] [--spp 16] [--passes 1]
 //              [--n-rays 16] [--depth 8] [--seed 20241223] [--device 0]
 //              [--out result.png] [--pfm pixels.pfm] [--counts counts.u32]
+//              [--pgm result.pgm] [--smooth SIDE] [--glare CUTOFF --glare-out glare.pfm]
+//
+// --smooth applies GridRenderPlane::smooth(SIDE) on the GPU before output;
+// --glare writes Gui's glare bloom of the plane (gui.cpp:28-52, GPU) as PFM;
+// --pgm writes main.cpp's contrast/gamma PGM (main.cpp:297-309).
 //
 // Prints one JSON line: scene, size, passes, Mpaths/s (whole call and kernel).
 #include <chrono>
@@ -26,13 +31,16 @@ namespace {
     std::fprintf(stderr,
                  "usage: ipt_render [--scene NAME] [--width W] [--height H] [--spp S] [--passes P]\n"
                  "                  [--n-rays N] [--depth D] [--seed X] [--device I]\n"
-                 "                  [--out result.png] [--pfm pixels.pfm] [--counts counts.u32]\n");
+                 "                  [--out result.png] [--pfm pixels.pfm] [--counts counts.u32]\n"
+                 "                  [--pgm result.pgm] [--smooth SIDE] [--glare CUTOFF --glare-out F.pfm]\n");
     std::exit(2);
 }
 }  // namespace
 
 int main(int argc, char** argv) {
-    std::string scene_name = "box", out = "result.png", pfm, counts;
+    std::string scene_name = "box", out = "result.png", pfm, counts, pgm, glare_out;
+    long smooth = 0;
+    double glare = -1.0;
     long width = 640, height = 640, spp = 16, passes = 1, n_rays = 16, depth = 8, device = 0;
     unsigned long long seed = 20241223ull;
     for (int i = 1; i < argc; ++i) {
@@ -53,6 +61,10 @@ int main(int argc, char** argv) {
         else if (a == "--out") out = val();
         else if (a == "--pfm") pfm = val();
         else if (a == "--counts") counts = val();
+        else if (a == "--pgm") pgm = val();
+        else if (a == "--smooth") smooth = std::atol(val());
+        else if (a == "--glare") glare = std::atof(val());
+        else if (a == "--glare-out") glare_out = val();
         else usage(("unknown option " + a).c_str());
     }
     if (width <= 0 || height <= 0 || spp <= 0 || passes <= 0 || n_rays < 0 || depth < 0) usage("bad sizes");
@@ -76,6 +88,13 @@ int main(int argc, char** argv) {
             kernel_ms += pm + am;
         }
         const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (smooth > 0) gpu.smooth(plane, (size_t)smooth);
+        if (glare >= 0.0 && !glare_out.empty()) {
+            ipt::GridRenderPlane g(plane.width, plane.height);
+            g.pixels = gpu.glare(plane, (float)glare);
+            ipt::write_pfm(glare_out, g);
+        }
+        if (!pgm.empty()) ipt::write_pgm(pgm, plane);
         if (!out.empty()) ipt::write_png_gray8(out, plane.width, plane.height, ipt::to_gray8(plane));
         if (!pfm.empty()) ipt::write_pfm(pfm, plane);
         if (!counts.empty()) {

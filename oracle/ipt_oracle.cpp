@@ -802,3 +802,56 @@ float ipt_oracle_cosine_ddf_value(const float* to, const float* d) {
     return r.value(mk(d[0], d[1], d[2]));
 }
 }
+
+// ------------------------------------------------------------ post-process
+// Literal restatements of the reference's image post-process (SURVEY.md §8(f)
+// row 2), same loop order and types, for tests/test_post.py.
+extern "C" {
+// GridRenderPlane::smooth (in_place = 1) / computeSmoothedMax (in_place = 0),
+// GridRenderPlane.cpp:10-59: y, x downwards from the bottom-right, size_t
+// bounds `y >= side-1` (side 0: no iteration; side 1 would wrap: rejected).
+int ipt_oracle_smooth(float* pixels, size_t width, size_t height, size_t side, int in_place, float* max_out) {
+    if (side == 1) return -1;
+    float max_value = 0.0f;
+    if (height == 0 || width == 0) { *max_out = 0.0f; return 0; }
+    for (size_t y = height - 1; y >= side - 1; --y) {
+        for (size_t x = width - 1; x >= side - 1; --x) {
+            float accum = 0.0f;
+            for (size_t yy = 0; yy < side; ++yy)
+                for (size_t xx = 0; xx < side; ++xx) accum += pixels[(y - yy) * width + x - xx];
+            accum /= side * side;
+            if (in_place) pixels[y * width + x] = accum;
+            if (accum > max_value) max_value = accum;
+            if (x == 0) break;
+        }
+        if (y == 0) break;
+    }
+    *max_out = max_value;
+    return 0;
+}
+
+// gui.cpp:28-52: draw_halo(img, cx, cy, C, r0) adds C/(r0+r)/(r0+r) with
+// r = (float)hypot(x-cx, y-cy) to every pixel; glare copies the image, draws a
+// halo of C = cutoff*(float)(0.1*val/cutoff) for every pixel with
+// !(val <= cutoff) in raster order, then cuts to [0, cutoff].
+void ipt_oracle_glare(const float* img, float* out, int width, int height, float cutoff) {
+    std::vector<float> o(img, img + (size_t)width * height);
+    for (int y = 0; y < height; ++y)
+        for (int x = 0; x < width; ++x) {
+            float val = img[(size_t)y * width + x];
+            if (val <= cutoff) continue;
+            float coef = 0.1 * val / cutoff;
+            const float C = cutoff * coef, r0 = 0.25f;
+            for (int yy = 0; yy < height; ++yy)
+                for (int xx = 0; xx < width; ++xx) {
+                    float r = std::hypot(xx - x, yy - y);
+                    float v = C / (r0 + r) / (r0 + r);
+                    o[(size_t)yy * width + xx] += v;
+                }
+        }
+    for (size_t i = 0; i < o.size(); ++i) {
+        const float v = o[i];
+        out[i] = v < 0.0f ? 0.0f : (v > cutoff ? cutoff : v);
+    }
+}
+}

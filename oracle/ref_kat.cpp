@@ -295,6 +295,30 @@ int main(int argc, char** argv) {
         out.push_back(g.max_value);
         write("ref_grid.bin", out);
     }
+    // 10. GridRenderPlane::smooth(side) and computeSmoothedMax(side)
+    //     (GridRenderPlane.cpp:10-59) on random planes (some zero pixels):
+    //     per case W H side, input pixels, smoothed pixels, smooth's max,
+    //     computeSmoothedMax's max (on the unsmoothed input)
+    {
+        std::vector<float> out;
+        const int cases[][3] = {{37, 23, 2}, {37, 23, 3}, {16, 40, 5}, {9, 9, 9}, {8, 6, 7}, {5, 5, 0}};
+        out.push_back((float)(sizeof(cases) / sizeof(cases[0])));
+        for (const auto& c : cases) {
+            const int W = c[0], H = c[1], side = c[2];
+            GridRenderPlane g(W, H), h(W, H);
+            for (int i = 0; i < W * H; ++i) g.pixels[i] = h.pixels[i] = (rng() % 7 == 0) ? 0.0f : U(0, 30);
+            out.push_back((float)W);
+            out.push_back((float)H);
+            out.push_back((float)side);
+            out.insert(out.end(), g.pixels.begin(), g.pixels.end());
+            g.smooth(side);
+            h.computeSmoothedMax(side);
+            out.insert(out.end(), g.pixels.begin(), g.pixels.end());
+            out.push_back(g.max_value);
+            out.push_back(h.max_value);
+        }
+        write("ref_smooth.bin", out);
+    }
     std::printf("ref_kat: fixtures written to %s\n", g_dir.c_str());
     return 0;
 }

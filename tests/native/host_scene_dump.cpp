@@ -59,6 +59,16 @@ int main(int argc, char** argv) {
         ipt::write_png_gray8(argv[5], w, h, ipt::to_gray8(plane));
         return 0;
     }
-    std::fprintf(stderr, "usage: host_scene_dump scene NAME | scene-error NAME | gray8 W H in.f32 out.png\n");
+    if (argc >= 7 && std::strcmp(argv[1], "pgm") == 0) {
+        const size_t w = std::strtoul(argv[2], nullptr, 10), h = std::strtoul(argv[3], nullptr, 10);
+        ipt::GridRenderPlane plane(w, h);
+        std::ifstream in(argv[4], std::ios::binary);
+        in.read(reinterpret_cast<char*>(plane.pixels.data()), (std::streamsize)(w * h * 4));
+        plane.max_value = std::strtof(argv[5], nullptr);
+        ipt::write_pgm(argv[6], plane);
+        return 0;
+    }
+    std::fprintf(stderr, "usage: host_scene_dump scene NAME | scene-error NAME | gray8 W H in.f32 out.png | "
+                         "pgm W H in.f32 MAX out.pgm\n");
     return 2;
 }

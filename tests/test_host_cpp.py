@@ -4,6 +4,7 @@ its scenes must be bit-identical to the Python builders the parity tests use
 (ipt_amd/scenes.py), and its 8-bit output must follow gui.cpp/CImg's
 normalisation. The GPU half (ipt_render CLI vs the oracle image) is
 tests/test_gpu_parity.py::test_cli_render_matches_oracle."""
+import ctypes as C
 import json
 import struct
 import subprocess
@@ -99,6 +100,35 @@ def test_gray8_png_follows_gui_save(dump, tmp_path):
     m, M = v.min(), v.max()
     v = ((v - m) / (M - m) * np.float32(255.0)).astype(np.float32)
     assert np.array_equal(got.reshape(-1), v.astype(np.uint8))
+
+
+def test_pgm_follows_main_cpp(dump, tmp_path):
+    """main.cpp:225-235,297-309: n_val with contrast 500, gamma 0.6, float
+    logf/powf (the reference's `using namespace std` overloads), ASCII P2."""
+    libm = C.CDLL("libm.so.6")
+    libm.logf.restype = libm.powf.restype = C.c_float
+    libm.logf.argtypes = [C.c_float]
+    libm.powf.argtypes = [C.c_float, C.c_float]
+    rng = np.random.default_rng(9)
+    W, H = 13, 7
+    px = (rng.random(W * H, dtype=np.float32) * np.float32(2.0)).astype(np.float32)
+    px.tofile(tmp_path / "p.f32")
+    mx = float(px.max())
+    subprocess.run([str(dump), "pgm", str(W), str(H), str(tmp_path / "p.f32"), repr(mx), str(tmp_path / "o.pgm")],
+                   check=True)
+    txt = (tmp_path / "o.pgm").read_text().split()
+    assert txt[:4] == ["P2", str(W), str(H), "255"]
+    contrast, gamma = np.float32(500.0), np.float32(0.6)
+    exp = []
+    for v in px:
+        adj = np.float32(np.float32(v * contrast) / np.float32(mx))
+        adj = min(adj, contrast)
+        adj = max(adj, np.float32(1.0))
+        fn = np.float32(np.float32(libm.logf(adj)) / np.float32(libm.logf(contrast)))
+        fn = np.float32(libm.powf(fn, gamma))
+        n = int(np.float32(256) * fn)
+        exp.append(str(min(255, max(0, n))))
+    assert txt[4:] == exp
 
 
 def test_cli_requires_gpu():
