@@ -194,6 +194,24 @@ int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
 int ipt_smooth(ipt_ctx* ctx, float* pixels, int width, int height, int side, int in_place, float* max_value);
 int ipt_glare(ipt_ctx* ctx, const float* in, float* out, int width, int height, float cutoff);
 
+/* ---- the path's DDF samplers, exactly as the kernels evaluate them -----------
+   For sampler validation (the reference's chi^2 harness, check_ddf.cpp:114-203)
+   and bit-exact checks. Uses the uploaded scene. kind:
+     IPT_DDF_COSINE  RotateDdf(CosineDdf, to): params = to[3]
+     IPT_DDF_LIGHT   DdfFromLight (lighting.cpp:38-73) of scene light params[3]
+                     at origin params[0..2]
+     IPT_DDF_MIXTURE UnionDdf(lights..., RotateDdf(CosineDdf, normal)) with
+                     the scene's unite() weights: origin params[0..2], normal
+                     params[3..5]
+   ipt_ddf_sample: u = n x {pick, u1, u2} uniforms in [0,1) -> n directions
+   (vec3() where the reference's sampler returns it); ipt_ddf_value: n
+   directions -> n DDF values. Host buffers. */
+#define IPT_DDF_COSINE 0
+#define IPT_DDF_LIGHT 1
+#define IPT_DDF_MIXTURE 2
+int ipt_ddf_sample(ipt_ctx* ctx, int kind, const float* params, const float* u, int64_t n, float* dirs);
+int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs, int64_t n, float* values);
+
 /* ---- portable-math probes (same code as the kernels), for tests ---------
    fn: 0 acosf, 1 sinf, 2 cosf, 3 (float)acos((double)x), 4 sincosf->sin,
        5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u),

@@ -18,6 +18,7 @@ LIB_PATH = _HERE / "lib" / "libipt_hip.so"
 
 IPT_OK = 0
 IPT_E_INVALID = -1
+IPT_DDF_COSINE, IPT_DDF_LIGHT, IPT_DDF_MIXTURE = 0, 1, 2
 IPT_E_DEVICE = -2
 IPT_E_UNSUPPORTED = -3
 IPT_E_NOSCENE = -4
@@ -81,7 +82,7 @@ EXPORTED_SYMBOLS = (
     "ipt_abi_version", "ipt_last_error", "ipt_create", "ipt_destroy", "ipt_upload_scene",
     "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
-    "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck", "ipt_smooth", "ipt_glare",
+    "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck", "ipt_smooth", "ipt_glare", "ipt_ddf_sample", "ipt_ddf_value",
 )
 
 # path-kernel phases of the IPT_PROF profile (ipt_kernels.hip IPT_PHASE ids)
@@ -125,6 +126,8 @@ def load(path: str | os.PathLike | None = None):
     lib.ipt_reset_counters.argtypes = [C.c_void_p]
     lib.ipt_math_selfcheck.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_uint64,
                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    lib.ipt_ddf_sample.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+    lib.ipt_ddf_value.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
     lib.ipt_smooth.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                C.POINTER(C.c_float)]
     lib.ipt_glare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_float]
@@ -249,6 +252,23 @@ class Context:
         _check(self.lib, self.h, self.lib.ipt_math_selfcheck(self.h, fn, lo_bits, hi_bits, C.byref(bad),
                                                              C.byref(first)))
         return int(bad.value), int(first.value)
+
+    def ddf_sample(self, kind: int, params, u: np.ndarray) -> np.ndarray:
+        """n directions from n x {pick, u1, u2} uniforms (ipt_ddf_sample)."""
+        pr = np.ascontiguousarray(np.pad(np.asarray(params, np.float32), (0, 8))[:8])
+        uu = np.ascontiguousarray(u, np.float32).reshape(-1, 3)
+        out = np.empty((len(uu), 3), np.float32)
+        _check(self.lib, self.h, self.lib.ipt_ddf_sample(self.h, kind, pr.ctypes.data, uu.ctypes.data, len(uu),
+                                                         out.ctypes.data))
+        return out
+
+    def ddf_value(self, kind: int, params, dirs: np.ndarray) -> np.ndarray:
+        pr = np.ascontiguousarray(np.pad(np.asarray(params, np.float32), (0, 8))[:8])
+        dd = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        out = np.empty(len(dd), np.float32)
+        _check(self.lib, self.h, self.lib.ipt_ddf_value(self.h, kind, pr.ctypes.data, dd.ctypes.data, len(dd),
+                                                        out.ctypes.data))
+        return out
 
     def smooth(self, pixels: np.ndarray, width: int, height: int, side: int, in_place: bool = True):
         """GridRenderPlane::smooth (in_place) / computeSmoothedMax on the GPU:

@@ -944,6 +944,56 @@ __global__ void math_kernel(int fn, const float* in, float* out, long long n) {
     if (i < n) out[i] = math_fn(fn, in[i]);
 }
 
+// DDF samplers / values exactly as the path kernel evaluates them, for the
+// sampler checks (ipt_ddf_sample / ipt_ddf_value; tests/test_ddf_samplers.py).
+// kind 0: RotateDdf(CosineDdf, to=params[0..2]); kind 1: DdfFromLight of light
+// params[3] at origin params[0..2]; kind 2: the UnionDdf of every light and
+// RotateDdf(CosineDdf, normal=params[3..5]) at origin params[0..2].
+__global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ params, const LightDev* __restrict__ lights,
+                           const float* __restrict__ weights, const float* __restrict__ cdf, int nl,
+                           const float* __restrict__ in, long long n, float* __restrict__ out) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const vec3 o = v3(params[0], params[1], params[2]);
+    if (!value_mode) {
+        const float pick = in[3 * i], u1 = in[3 * i + 1], u2 = in[3 * i + 2];
+        vec3 v = v3(0.0f, 0.0f, 0.0f);
+        if (kind == 0) {
+            v = frame_apply(make_frame(o), cosine_sample_local(u1, u2));
+        } else if (kind == 1) {
+            v = light_sample_dir(lights[(int)params[3]], o, u1, u2);
+        } else {
+            int c = 0;
+            while (c <= nl && !(pick < cdf[c])) ++c;
+            if (c < nl) v = light_sample_dir(lights[c], o, u1, u2);
+            else if (c == nl) v = frame_apply(make_frame(v3(params[3], params[4], params[5])), cosine_sample_local(u1, u2));
+        }
+        out[3 * i] = v.x;
+        out[3 * i + 1] = v.y;
+        out[3 * i + 2] = v.z;
+    } else {
+        const vec3 d = v3(in[3 * i], in[3 * i + 1], in[3 * i + 2]);
+        float v;
+        if (kind == 0) {
+            v = frame_cosine_value(make_frame(o), d);
+        } else if (kind == 1) {
+            const LightDev& L = lights[(int)params[3]];
+            vec3 hp;
+            const bool h = light_trace(L, o, d, &hp);
+            v = light_pdf(L, o, h, hp);
+        } else {
+            float lmix = 0.0f;
+            for (int l = 0; l < nl; ++l) {
+                vec3 hp;
+                const bool h = light_trace(lights[l], o, d, &hp);
+                lmix += weights[l] * light_pdf(lights[l], o, h, hp);
+            }
+            v = lmix + weights[nl] * frame_cosine_value(make_frame(v3(params[3], params[4], params[5])), d);
+        }
+        out[i] = v;
+    }
+}
+
 // Exact restatement of math_fn (differs only where the device uses a fast
 // path, i.e. fn 3): the reference for ipt_math_selfcheck.
 __device__ float math_fn_exact(int fn, float x) {
@@ -1578,6 +1628,43 @@ int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n
     hipFree(din);
     hipFree(dout);
     return IPT_OK;
+}
+
+static int ddf_call(ipt_ctx* ctx, int value_mode, int kind, const float* params, const float* in, int64_t n,
+                    float* out) {
+    if (!ctx) return IPT_E_INVALID;
+    if (!params || !in || !out || n < 0 || kind < 0 || kind > 2) return fail(ctx, IPT_E_INVALID, "ipt_ddf: bad arguments");
+    if (!ctx->has_scene) return fail(ctx, IPT_E_INVALID, "ipt_ddf: no scene uploaded");
+    if (kind == 1 && (params[3] < 0.0f || params[3] >= (float)ctx->n_lights || params[3] != (float)(int)params[3]))
+        return fail(ctx, IPT_E_INVALID, "ipt_ddf: light index out of range");
+    hipSetDevice(ctx->device);
+    const size_t in_w = 3, out_w = value_mode ? 1 : 3;
+    float *dp = nullptr, *din = nullptr, *dout = nullptr;
+    HIPCHECK(ctx, hipMalloc(&dp, 8 * sizeof(float)));
+    HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * in_w * sizeof(float)));
+    HIPCHECK(ctx, hipMalloc(&dout, std::max<int64_t>(n, 1) * out_w * sizeof(float)));
+    float hp[8] = {0};
+    for (int k = 0; k < (kind == 0 ? 3 : (kind == 1 ? 4 : 6)); ++k) hp[k] = params[k];
+    HIPCHECK(ctx, hipMemcpy(dp, hp, sizeof hp, hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(din, in, n * in_w * sizeof(float), hipMemcpyHostToDevice));
+    if (n > 0)
+        hipLaunchKernelGGL(ddf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, value_mode, kind,
+                           dp, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->n_lights, din, (long long)n, dout);
+    HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHECK(ctx, hipMemcpy(out, dout, n * out_w * sizeof(float), hipMemcpyDeviceToHost));
+    hipFree(dp);
+    hipFree(din);
+    hipFree(dout);
+    return IPT_OK;
+}
+
+int ipt_ddf_sample(ipt_ctx* ctx, int kind, const float* params, const float* u, int64_t n, float* dirs) {
+    return ddf_call(ctx, 0, kind, params, u, n, dirs);
+}
+
+int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs, int64_t n, float* values) {
+    return ddf_call(ctx, 1, kind, params, dirs, n, values);
 }
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,

@@ -135,7 +135,11 @@ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
         k1 += 0xBB67AE85u;
     }
 }
+// Test hook: when set, randf() returns these uniforms in order instead of the
+// Philox stream (explicit-uniform sampler checks, ipt_oracle_ddf_sample).
+thread_local const float* g_ufeed = nullptr;
 float randf() {
+    if (g_ufeed) return *g_ufeed++;
     Rng& g = *g_rng;
     uint32_t b = g.k >> 2;
     if (b != g.blk_id) {
@@ -853,5 +857,77 @@ void ipt_oracle_glare(const float* img, float* out, int width, int height, float
         const float v = o[i];
         out[i] = v < 0.0f ? 0.0f : (v > cutoff ? cutoff : v);
     }
+}
+}
+
+// ---------------------------------------------------------------- DDFs
+// The three samplers of the path with explicit uniforms (3 per sample: pick,
+// u1, u2), for tests/test_ddf_samplers.py (device parity + the reference's
+// chi^2 harness check_ddf.cpp:114-203). kind 0: RotateDdf(CosineDdf, to),
+// params = to; kind 1: DdfFromLight of light params[3] at origin params[0..2]
+// (lighting.cpp:125-148); kind 2: UnionDdf of all lights + RotateDdf(CosineDdf,
+// normal) with the scene's unite() weights (ddf.cpp:142-162), origin
+// params[0..2], normal params[3..5].
+namespace {
+V3 light_ddf_sample(const AreaLightO& l, V3 o) {
+    V3 pos, n;
+    float sp;
+    l.sample(&pos, &n, &sp);
+    V3 dir = normalize(pos - o);
+    if (dot(n, -dir) < 1e-5f) return mk(0.0f, 0.0f, 0.0f);  // lighting.cpp:130-131
+    return dir;
+}
+}  // namespace
+extern "C" {
+int ipt_oracle_ddf_sample(const ipt_scene* scene, int kind, const float* params, const float* u, int n,
+                          float* out3n) {
+    SceneO sc = make_scene(scene);
+    const V3 o = mk(params[0], params[1], params[2]);
+    Mixture mx = build_mixture(sc);
+    for (int i = 0; i < n; ++i) {
+        V3 v = mk(0.0f, 0.0f, 0.0f);
+        if (kind == 0) {
+            g_ufeed = u + 3 * i + 1;
+            v = RotatedCosine(o).sample();
+        } else if (kind == 1) {
+            g_ufeed = u + 3 * i + 1;
+            v = light_ddf_sample(sc.lights[(int)params[3]], o);
+        } else {
+            g_ufeed = u + 3 * i;
+            const float r = randf();  // UnionDdf::sample: first r < running sum
+            float acc = 0.0f;
+            size_t c = 0;
+            for (; c < mx.weights.size(); ++c) {
+                acc += mx.weights[c];
+                if (r < acc) break;
+            }
+            if (c < sc.lights.size()) v = light_ddf_sample(sc.lights[c], o);
+            else if (c == sc.lights.size()) v = RotatedCosine(mk(params[3], params[4], params[5])).sample();
+        }
+        g_ufeed = nullptr;
+        out3n[3 * i] = v.x; out3n[3 * i + 1] = v.y; out3n[3 * i + 2] = v.z;
+    }
+    return 0;
+}
+int ipt_oracle_ddf_value(const ipt_scene* scene, int kind, const float* params, const float* dirs, int n,
+                         float* out) {
+    SceneO sc = make_scene(scene);
+    const V3 o = mk(params[0], params[1], params[2]);
+    Mixture mx = build_mixture(sc);
+    for (int i = 0; i < n; ++i) {
+        const V3 d = mk(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        float v;
+        if (kind == 0) {
+            v = RotatedCosine(o).value(d);
+        } else if (kind == 1) {
+            v = light_ddf_value(sc.lights[(int)params[3]], o, d);
+        } else {
+            v = 0.0f;  // UnionDdf::value: sequential sum in component order
+            for (size_t c = 0; c < sc.lights.size(); ++c) v += mx.weights[c] * light_ddf_value(sc.lights[c], o, d);
+            v += mx.weights.back() * RotatedCosine(mk(params[3], params[4], params[5])).value(d);
+        }
+        out[i] = v;
+    }
+    return 0;
 }
 }
