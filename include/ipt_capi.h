@@ -45,7 +45,15 @@ enum {
     /* The same five box planes followed by N extra spheres scanned in order
        with FractalSpheres' acceptance rule (FractalSpheres.cpp:75-84); the
        10k-primitive stress configuration of BASELINE.json configs[2]. */
-    IPT_GEOM_SPHERES_IN_BOX = 1
+    IPT_GEOM_SPHERES_IN_BOX = 1,
+    /* GeometryFloor (GeometryFloor.cpp:10-23): the z = -1 face of the cube
+       ([-1,1]^2 through intersection_with_box_plane), unrotated CosineDdf.
+       sample_scenes' make_scene_square_lit_by_square. */
+    IPT_GEOM_FLOOR = 2,
+    /* GeometryCorner (GeometryCorner.cpp:10-42): the x = -1, y = -1, z = -1
+       faces, strict-< nearest in that order, RotateDdf(CosineDdf, normal).
+       sample_scenes' make_scene_lit_corner. */
+    IPT_GEOM_CORNER = 3
 };
 
 /* Light kinds (reference src/lighting/lighting.h). */

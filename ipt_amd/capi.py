@@ -26,6 +26,8 @@ IPT_E_OOM = -5
 
 IPT_GEOM_SPHERE_IN_BOX = 0
 IPT_GEOM_SPHERES_IN_BOX = 1
+IPT_GEOM_FLOOR = 2
+IPT_GEOM_CORNER = 3
 IPT_LIGHT_AREA_DIAMOND = 0
 IPT_LIGHT_AREA_TRIANGLE = 1
 IPT_FLAG_COUNTERS = 1

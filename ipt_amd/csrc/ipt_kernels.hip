@@ -168,6 +168,21 @@ template <bool COUNT, int GEOM>
 __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim, uint32_t& c_nodes,
                                                 uint32_t& c_tests) {
     if (GEOM == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
+    if (GEOM == IPT_GEOM_FLOOR) {  // GeometryFloor.cpp:11-13
+        const float t = box_plane_t(o.z, d.z, -1.0f, o, d);
+        *prim = t == inf_() ? -1 : 0;
+        return t;
+    }
+    if (GEOM == IPT_GEOM_CORNER) {  // GeometryCorner.cpp:11-28: tx, then ty, tz with strict <
+        float t = box_plane_t(o.x, d.x, -1.0f, o, d);
+        int p = 0;
+        const float ty = box_plane_t(o.y, d.y, -1.0f, o, d);
+        if (ty < t) { t = ty; p = 1; }
+        const float tz = box_plane_t(o.z, d.z, -1.0f, o, d);
+        if (tz < t) { t = tz; p = 2; }
+        *prim = t == inf_() ? -1 : p;
+        return t;
+    }
     // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
     // (FractalSpheres.cpp:75-84): strict '<' in index order == minimal t,
     // lowest index among equal t, and a sphere never wins a tie with a plane.
@@ -1180,9 +1195,12 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
 }
 template <int MAXSUSP, bool COUNT, int LMODE>
 int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
-    if (kp.geometry_kind == IPT_GEOM_SPHERES_IN_BOX)
-        return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES_IN_BOX>(ctx, kp, st);
-    return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+    switch (kp.geometry_kind) {
+        case IPT_GEOM_SPHERES_IN_BOX: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES_IN_BOX>(ctx, kp, st);
+        case IPT_GEOM_FLOOR: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_FLOOR>(ctx, kp, st);
+        case IPT_GEOM_CORNER: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_CORNER>(ctx, kp, st);
+        default: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+    }
 }
 template <int MAXSUSP, bool COUNT>
 int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
@@ -1373,7 +1391,7 @@ void ipt_destroy(ipt_ctx* ctx) {
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!ctx) return IPT_E_INVALID;
     if (!s) return fail(ctx, IPT_E_INVALID, "scene is NULL");
-    if (s->geometry_kind != IPT_GEOM_SPHERE_IN_BOX && s->geometry_kind != IPT_GEOM_SPHERES_IN_BOX)
+    if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_CORNER)
         return fail(ctx, IPT_E_UNSUPPORTED, "unknown geometry_kind");
     if (s->n_lights < 0 || s->n_lights > kMaxLights || (s->n_lights > 0 && !s->lights))
         return fail(ctx, IPT_E_UNSUPPORTED, "n_lights out of range");
@@ -1399,10 +1417,17 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         acc += wts[i];  // UnionDdf::sample's running sum (ddf.cpp:145-146)
         cdf[i] = acc;
     }
-    // wall frames: RotateDdf(CosineDdf, -plane) for planes {+x,+y,+z,-x,-z}
+    // plane frames, indexed by the plane primitive the geometry trace returns:
+    // box: RotateDdf(CosineDdf, -plane) for planes {+x,+y,+z,-x,-z};
+    // corner: RotateDdf(CosineDdf, n) for n = +x, +y, +z (GeometryCorner.cpp:16-28);
+    // floor: its unrotated CosineDdf == make_frame((0,0,1)), which is exactly
+    // the identity (axis falls back to +x, angle acos(1) = 0, sin 0 = 0, cos 0 = 1)
     const vec3 planes[5] = {v3(1, 0, 0), v3(0, 1, 0), v3(0, 0, 1), v3(-1, 0, 0), v3(0, 0, -1)};
     Frame wall[5];
     for (int i = 0; i < 5; ++i) wall[i] = make_frame(-planes[i]);
+    if (s->geometry_kind == IPT_GEOM_CORNER)
+        for (int i = 0; i < 3; ++i) wall[i] = make_frame(planes[i]);
+    if (s->geometry_kind == IPT_GEOM_FLOOR) wall[0] = make_frame(v3(0, 0, 1));
     std::vector<float4> sph(std::max(s->n_spheres, 1));
     for (int i = 0; i < s->n_spheres; ++i)
         sph[i] = make_float4(s->spheres[i].center[0], s->spheres[i].center[1], s->spheres[i].center[2], s->spheres[i].radius);

@@ -138,10 +138,30 @@ Scene make_scene_random_lights(int n, uint64_t seed) {
     return Scene{std::make_shared<GeometrySphereInBox>(), lighting, box_camera()};
 }
 
+Scene make_scene_square_lit_by_square() {
+    auto lighting = std::make_shared<CollectionLighting>();
+    lighting->addSquareLight(vec3f{-0.05f, -0.05f, -0.9f}, vec3f{0, 0, -1}, vec3f{0, 0.1f, 0});
+    const vec3 camera_pos = v3(0, -5.0f, 0);
+    const vec3 camera_dir = normalize(v3(0, 0, -1.0f) - camera_pos);
+    auto camera = std::make_shared<SimpleCamera>(h(camera_pos), h(camera_dir * 2.0f), vec3f{0, 1, 0});
+    return Scene{std::make_shared<GeometryFloor>(), lighting, camera};
+}
+
+Scene make_scene_lit_corner() {
+    auto lighting = std::make_shared<CollectionLighting>();
+    const vec3 out = v3(1, 1, 1);
+    const vec3 cx = v3(-0.5f, -1.0f, -1.0f) + 0.5f * out;
+    const vec3 cy = v3(-1.0f, -0.5f, -1.0f) + 0.5f * out;
+    const vec3 cz = v3(-1.0f, -1.0f, -0.5f) + 0.5f * out;
+    lighting->addTriangleLight(h(cx), h(cz - cx), h(cy - cx));
+    const vec3 camera_pos = v3(4.0f, 1.0f, 1.0f);
+    const vec3 camera_dir = normalize(v3(0, 0, 0.0f) - camera_pos);
+    return Scene{std::make_shared<GeometryCorner>(), lighting,
+                 std::make_shared<SimpleCamera>(h(camera_pos), h(camera_dir))};
+}
+
 Scene make_scene_fractal() { unsupported("make_scene_fractal (FractalSpheres + SphereLight)"); }
 Scene make_scene_smallpt() { unsupported("make_scene_smallpt (GeometrySmallPt)"); }
-Scene make_scene_square_lit_by_square() { unsupported("make_scene_square_lit_by_square (GeometryFloor)"); }
-Scene make_scene_lit_corner() { unsupported("make_scene_lit_corner (GeometryCorner)"); }
 
 Scene make_scene_by_name(const std::string& spec) {
     std::vector<std::string> f;
@@ -170,6 +190,10 @@ FlatScene flatten(const Scene& s) {
     if (!s.geometry || !s.lighting || !s.camera) throw IptError(IPT_E_INVALID, "scene has a null member");
     if (dynamic_cast<const GeometrySphereInBox*>(s.geometry.get())) {
         out.scene.geometry_kind = IPT_GEOM_SPHERE_IN_BOX;
+    } else if (dynamic_cast<const GeometryFloor*>(s.geometry.get())) {
+        out.scene.geometry_kind = IPT_GEOM_FLOOR;
+    } else if (dynamic_cast<const GeometryCorner*>(s.geometry.get())) {
+        out.scene.geometry_kind = IPT_GEOM_CORNER;
     } else if (auto sp = dynamic_cast<const SpheresInBox*>(s.geometry.get())) {
         out.scene.geometry_kind = IPT_GEOM_SPHERES_IN_BOX;
         for (const auto& q : sp->spheres) {

@@ -17,8 +17,8 @@
 // the CPU. Rendering is GpuRenderer / render_samples_gpu, i.e. ipt_render on
 // a gfx950 GPU, and it throws IptError(IPT_E_DEVICE) when there is none.
 // Scene types the GPU kernels do not implement yet (§8(f) row 1: point,
-// sphere and outer lights, the fractal / smallpt / floor / corner scenes)
-// throw IptError(IPT_E_UNSUPPORTED) where they are created.
+// sphere and outer lights, the fractal / smallpt scenes) throw
+// IptError(IPT_E_UNSUPPORTED) where they are created.
 #pragma once
 
 #include <cstddef>
@@ -58,6 +58,11 @@ struct SpheresInBox : Geometry {
     };
     std::vector<Sphere> spheres;
 };
+
+// The z = -1 face (GeometryFloor.cpp:10-23), unrotated CosineDdf.
+struct GeometryFloor : Geometry {};
+// The x = -1, y = -1, z = -1 faces (GeometryCorner.cpp:10-42).
+struct GeometryCorner : Geometry {};
 
 // ------------------------------------------------------------- lighting
 struct Light {
@@ -121,11 +126,11 @@ Scene make_scene_box();                                   // sample_scenes[0]
 Scene make_scene_box_lights(int k);                       // [0]'s light as k*k squares (C5: k=16)
 Scene make_scene_spheres(int n, uint64_t seed = 1);       // box + n spheres (C3: n=10000)
 Scene make_scene_random_lights(int n, uint64_t seed = 7);  // overlapping random emitters (tests)
-// sample_scenes[1..4]: geometry/light types not on the GPU path yet (§8(f) row 1)
+Scene make_scene_square_lit_by_square();                  // sample_scenes.cpp:73-85
+Scene make_scene_lit_corner();                            // sample_scenes.cpp:88-108
+// not on the GPU path yet (§8(f) row 1): throw IptError(IPT_E_UNSUPPORTED)
 Scene make_scene_fractal();
 Scene make_scene_smallpt();
-Scene make_scene_square_lit_by_square();
-Scene make_scene_lit_corner();
 // "box", "box_lights:K", "spheres:N[:SEED]", "random_lights:N[:SEED]", "fractal", ...
 Scene make_scene_by_name(const std::string& name);
 

@@ -14,8 +14,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .capi import (IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES_IN_BOX, IPT_LIGHT_AREA_DIAMOND,
-                   IPT_LIGHT_AREA_TRIANGLE)
+from .capi import (IPT_GEOM_CORNER, IPT_GEOM_FLOOR, IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES_IN_BOX,
+                   IPT_LIGHT_AREA_DIAMOND, IPT_LIGHT_AREA_TRIANGLE)
 
 f32 = np.float32
 
@@ -76,6 +76,32 @@ def make_scene_box():
     light = square_light(box_light_corner(), (0.0, 0.0, -1.0), (0.0, 0.2, 0.0), 1.0)
     return {"geometry_kind": IPT_GEOM_SPHERE_IN_BOX, "lights": [light], "spheres": [],
             "camera": box_camera()}
+
+
+def make_scene_square_lit_by_square():
+    """sample_scenes.cpp:73-85: GeometryFloor lit by a 0.1 square, camera at
+    (0,-5,0) looking at (0,0,-1), direction scaled by 2, up hint +y."""
+    light = square_light((-0.05, -0.05, -0.9), (0.0, 0.0, -1.0), (0.0, 0.1, 0.0), 1.0)
+    camera_pos = _v(0.0, -5.0, 0.0)
+    camera_dir = normalize((_v(0.0, 0.0, -1.0) - camera_pos).astype(f32))
+    cam = simple_camera(camera_pos, (camera_dir * f32(2.0)).astype(f32), up_hint=(0.0, 1.0, 0.0))
+    return {"geometry_kind": IPT_GEOM_FLOOR, "lights": [light], "spheres": [], "camera": cam}
+
+
+def make_scene_lit_corner():
+    """sample_scenes.cpp:88-108: GeometryCorner lit by a triangle light
+    (addTriangleLight(cx, cz-cx, cy-cx)), camera at (4,1,1) looking at 0."""
+    out = _v(1.0, 1.0, 1.0)
+    half = (f32(0.5) * out).astype(f32)
+    cx = (_v(-0.5, -1.0, -1.0) + half).astype(f32)
+    cy = (_v(-1.0, -0.5, -1.0) + half).astype(f32)
+    cz = (_v(-1.0, -1.0, -0.5) + half).astype(f32)
+    light = {"position": cx.tolist(), "x_axis": (cz - cx).astype(f32).tolist(),
+             "y_axis": (cy - cx).astype(f32).tolist(), "power": 1.0, "type": IPT_LIGHT_AREA_TRIANGLE}
+    camera_pos = _v(4.0, 1.0, 1.0)
+    camera_dir = normalize((_v(0.0, 0.0, 0.0) - camera_pos).astype(f32))
+    return {"geometry_kind": IPT_GEOM_CORNER, "lights": [light], "spheres": [],
+            "camera": simple_camera(camera_pos, camera_dir)}
 
 
 def make_scene_box_lights(k: int = 16):

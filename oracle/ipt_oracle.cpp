@@ -255,6 +255,12 @@ float intersection_with_sphere(float radius, V3 origin, V3 direction) {
 // RotateDdf (ddf_detail.h:72-85) around a CosineDdf (ddf.cpp:223-238)
 struct RotatedCosine {
     M3 transformation, inv;
+    bool rotated = true;  // false: a plain CosineDdf (GeometryFloor's sdf, GeometryFloor.cpp:19)
+    static RotatedCosine plain() {
+        RotatedCosine r(mk(0.0f, 0.0f, 1.0f));
+        r.rotated = false;
+        return r;
+    }
     explicit RotatedCosine(V3 to) {
         V3 z = mk(0.0f, 0.0f, 1.0f);
         V3 axis = cross(z, to);
@@ -271,10 +277,10 @@ struct RotatedCosine {
         float phi = 2 * M_PI * u2;
         float r = std::sin(alpha);
         V3 x = mk(r * std::cos(phi), r * std::sin(phi), cos_alpha);
-        return mul(transformation, x);
+        return rotated ? mul(transformation, x) : x;
     }
     float value(V3 arg) const {
-        V3 a = mul(inv, arg);
+        V3 a = rotated ? mul(inv, arg) : arg;
         if (a.z < 0.0f) return 0.0f;
         return a.z / M_PI;
     }
@@ -282,11 +288,39 @@ struct RotatedCosine {
 
 struct SurfHit {
     V3 position, normal;
+    bool plain_cosine = false;  // unrotated CosineDdf (GeometryFloor)
 };
 // GeometrySphereInBox::traceRay (GeometrySphereInBox.cpp:10-81) and the
 // 5-planes + N-spheres stress geometry (FractalSpheres.cpp:69-97 acceptance).
 bool geometry_trace(const SceneO& sc, V3 origin, V3 direction, SurfHit* out) {
     if (g_cnt) ++g_cnt->traced;
+    if (sc.geometry_kind == IPT_GEOM_FLOOR) {  // GeometryFloor.cpp:10-23
+        float t = intersection_with_box_plane(mk(0, 0, -1), origin, direction);
+        if (t == INF || t < 0.0f || std::abs(t) < 1e-6) return false;
+        out->position = origin + direction * t;
+        out->normal = mk(0, 0, 1);
+        out->plain_cosine = true;
+        return true;
+    }
+    if (sc.geometry_kind == IPT_GEOM_CORNER) {  // GeometryCorner.cpp:10-42
+        float tx = intersection_with_box_plane(mk(-1, 0, 0), origin, direction);
+        float ty = intersection_with_box_plane(mk(0, -1, 0), origin, direction);
+        float tz = intersection_with_box_plane(mk(0, 0, -1), origin, direction);
+        float t = tx;
+        V3 normal = mk(1, 0, 0);
+        if (ty < t) {
+            t = ty;
+            normal = mk(0, 1, 0);
+        }
+        if (tz < t) {
+            t = tz;
+            normal = mk(0, 0, 1);
+        }
+        if (t == INF || t < 0.0f || std::abs(t) < 1e-6) return false;
+        out->position = origin + direction * t;
+        out->normal = normal;
+        return true;
+    }
     static const V3 planes[] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, 0, -1}};
     float dist = INF;
     int intersected_plane = -1;
@@ -421,8 +455,8 @@ float ray_power(const Ctx& cx, V3 origin, V3 direction, int depth, int n_rays) {
     }
     if (!has_si) return 0.0f;
     if (g_cnt) ++g_cnt->expanded;  // distributionInPoint call
-    // surface DDF: RotateDdf(CosineDdf, normal)
-    RotatedCosine sdf(si.normal);
+    // surface DDF: RotateDdf(CosineDdf, normal), or the floor's plain CosineDdf
+    RotatedCosine sdf = si.plain_cosine ? RotatedCosine::plain() : RotatedCosine(si.normal);
     if (g_cnt && !(si.normal.x == 0.0f && si.normal.y == 0.0f) &&
         !(si.normal.y == 0.0f && si.normal.z == 0.0f) && !(si.normal.x == 0.0f && si.normal.z == 0.0f))
         ++g_cnt->sframes;

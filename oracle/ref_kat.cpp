@@ -17,6 +17,8 @@
 #include "CollectionLighting.h"
 #include "lighting/lighting.h"
 #include "sample_scenes.h"
+#include "geometry/FractalSpheres.h"
+#include <functional>
 #include "libddf/ddf_detail.h"
 
 #include <cstdint>
@@ -28,6 +30,10 @@
 #include <vector>
 
 using glm::vec3;
+
+// FractalSpheres.cpp:16 (a free function the header does not declare)
+void generate_spheres(float r1, vec3 c1, float r2, vec3 c2, bool light_from_left,
+                      std::function<bool(float r, vec3 c)> callback);
 
 namespace {
 
@@ -318,6 +324,70 @@ int main(int argc, char** argv) {
             out.push_back(h.max_value);
         }
         write("ref_smooth.bin", out);
+    }
+    // 11. the other sample_scenes (sample_scenes.cpp:43-108): camera fields,
+    //     per light position/power/area, and light probes through the scene's
+    //     own traceRayToLight (AreaLight, triangle AreaLight, SphereLight)
+    {
+        std::vector<float> out;
+        Scene (*makers[])() = {make_scene_square_lit_by_square, make_scene_lit_corner, make_scene_fractal,
+                               make_scene_smallpt};
+        out.push_back(4.0f);
+        for (auto mk_scene : makers) {
+            Scene sc = mk_scene();
+            auto cam = std::dynamic_pointer_cast<const SimpleCamera>(sc.camera);
+            auto lit = std::dynamic_pointer_cast<const CollectionLighting>(sc.lighting);
+            float head[] = {cam->position.x, cam->position.y, cam->position.z, cam->direction.x,
+                            cam->direction.y, cam->direction.z, cam->right.x, cam->right.y, cam->right.z,
+                            cam->up.x, cam->up.y, cam->up.z, (float)lit->lights.size()};
+            out.insert(out.end(), head, head + 13);
+            for (auto& l : lit->lights) {
+                out.push_back(l->position.x);
+                out.push_back(l->position.y);
+                out.push_back(l->position.z);
+                out.push_back(l->power);
+                out.push_back(l->area);
+            }
+            for (int i = 0; i < 200; ++i) {
+                // aim at a point of the light (its own sample(), drand48) from a random origin
+                const vec3 t = lit->lights[0]->sample().position;
+                const float sc_len = glm::length(cam->position - t);
+                vec3 o = t + glm::normalize(vec3(U(-1, 1), U(-1, 1), U(-1, 1))) * U(0.05f, 1.0f) * sc_len;
+                vec3 d = glm::normalize(t - o);
+                auto hh = sc.lighting->traceRayToLight(o, d);
+                float rec[] = {o.x, o.y, o.z, d.x, d.y, d.z, hh ? 1.0f : 0.0f,
+                               hh ? hh->position.x : 0.f, hh ? hh->position.y : 0.f, hh ? hh->position.z : 0.f,
+                               hh ? hh->surface_power : 0.f};
+                out.insert(out.end(), rec, rec + 11);
+            }
+        }
+        write("ref_scenes.bin", out);
+    }
+    // 12. FractalSpheres' sphere list: the reference's generate_spheres
+    //     (FractalSpheres.cpp:16-44) driven as FractalSpheres::FractalSpheres
+    //     does (FractalSpheres.cpp:46-67: r1 = r2 = 0.5 at (-2,0,0), (2,0,0),
+    //     stop below r = 0.001); rs/cs are private, so the harness collects them
+    {
+        std::vector<float> rs, cs;
+        auto add_sphere = [&](float r, vec3 c) -> bool {
+            if (r < 0.001) return true;
+            rs.push_back(r);
+            cs.push_back(c.x);
+            cs.push_back(c.y);
+            cs.push_back(c.z);
+            return false;
+        };
+        add_sphere(0.5f, vec3(-2, 0, 0));
+        add_sphere(0.5f, vec3(2, 0, 0));
+        generate_spheres(0.5f, vec3(-2, 0, 0), 0.5f, vec3(2, 0, 0), true, add_sphere);
+        std::vector<float> out = {(float)rs.size()};
+        for (size_t i = 0; i < rs.size(); ++i) {
+            out.push_back(cs[3 * i]);
+            out.push_back(cs[3 * i + 1]);
+            out.push_back(cs[3 * i + 2]);
+            out.push_back(rs[i]);
+        }
+        write("ref_fractal_spheres.bin", out);
     }
     std::printf("ref_kat: fixtures written to %s\n", g_dir.c_str());
     return 0;

@@ -185,6 +185,20 @@ def test_light_bvh_active(gpu_ctx):
     assert c["light_traces"] >= 256 * c["traced_rays"]
 
 
+@pytest.mark.parametrize("name", ["make_scene_square_lit_by_square", "make_scene_lit_corner"])
+@pytest.mark.parametrize("n_rays,depth_max", [(16, 8), (4, 5)])
+def test_sample_scenes_floor_corner_bit_exact(gpu_ctx, oracle, name, n_rays, depth_max):
+    """sample_scenes.cpp:73-108: GeometryFloor (unrotated CosineDdf, identity
+    frame) with a square light; GeometryCorner (three faces, strict-<) with
+    a triangle light."""
+    desc = getattr(scenes, name)()
+    p = capi.make_params(40, 32, 2, n_rays=n_rays, depth_max=depth_max)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+    assert (ov > 0).mean() > 0.05  # the scene is lit
+
+
 def test_spheres_in_box_c3_scene(gpu_ctx, oracle):
     """The full 10k-sphere scene of BASELINE configs[2] (bench C3): BVH walk
     (octant orders, open-floor rays with best = inf) against the oracle's scan."""

@@ -52,13 +52,15 @@ def _py_flat(desc):
     ("box_lights:16", lambda: scenes.make_scene_box_lights(16)),
     ("spheres:300:1", lambda: scenes.make_scene_spheres(300, 1)),
     ("random_lights:17:7", lambda: scenes.make_scene_random_lights(17, 7)),
+    ("square_lit_by_square", scenes.make_scene_square_lit_by_square),
+    ("lit_corner", scenes.make_scene_lit_corner),
 ])
 def test_cpp_scenes_match_python(dump, name, desc_fn):
     out = subprocess.run([str(dump), "scene", name], check=True, capture_output=True, text=True).stdout
     assert json.loads(out) == _py_flat(desc_fn())
 
 
-@pytest.mark.parametrize("name", ["fractal", "smallpt", "square_lit_by_square", "lit_corner"])
+@pytest.mark.parametrize("name", ["fractal", "smallpt"])
 def test_unsupported_scenes_fail_loudly(dump, name):
     out = subprocess.run([str(dump), "scene-error", name], check=True, capture_output=True, text=True).stdout
     assert int(out) == capi.IPT_E_UNSUPPORTED
