@@ -53,11 +53,26 @@ enum {
     /* GeometryCorner (GeometryCorner.cpp:10-42): the x = -1, y = -1, z = -1
        faces, strict-< nearest in that order, RotateDdf(CosineDdf, normal).
        sample_scenes' make_scene_lit_corner. */
-    IPT_GEOM_CORNER = 3
+    IPT_GEOM_CORNER = 3,
+    /* FractalSpheres (FractalSpheres.cpp:69-97): the sphere list alone, no
+       walls, with the same acceptance rule as IPT_GEOM_SPHERES_IN_BOX.
+       sample_scenes' make_scene_fractal. */
+    IPT_GEOM_SPHERES = 4
 };
 
-/* Light kinds (reference src/lighting/lighting.h). */
-enum { IPT_LIGHT_AREA_DIAMOND = 0, IPT_LIGHT_AREA_TRIANGLE = 1 };
+/* Light kinds (reference src/lighting/lighting.h). Round lights use the
+   ipt_area_light record with position = centre and x_axis[0] = radius
+   (y_axis unused): SphereLight(centre, radius, power) (lighting.h:44-54),
+   PointLight(position, virtual_radius, power) (radius unused, lighting.h:
+   31-42), InvertedSphereLight(centre, radius, power) (addOuterLight,
+   lighting.h:57-72). */
+enum {
+    IPT_LIGHT_AREA_DIAMOND = 0,
+    IPT_LIGHT_AREA_TRIANGLE = 1,
+    IPT_LIGHT_SPHERE = 2,
+    IPT_LIGHT_POINT = 3,
+    IPT_LIGHT_OUTER_SPHERE = 4
+};
 
 /* AreaLight constructor arguments (lighting.cpp:79-90); derived fields
    (area, normal, inverse_matrix, surface power) are computed by

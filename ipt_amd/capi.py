@@ -28,8 +28,10 @@ IPT_GEOM_SPHERE_IN_BOX = 0
 IPT_GEOM_SPHERES_IN_BOX = 1
 IPT_GEOM_FLOOR = 2
 IPT_GEOM_CORNER = 3
+IPT_GEOM_SPHERES = 4
 IPT_LIGHT_AREA_DIAMOND = 0
 IPT_LIGHT_AREA_TRIANGLE = 1
+IPT_LIGHT_SPHERE, IPT_LIGHT_POINT, IPT_LIGHT_OUTER_SPHERE = 2, 3, 4
 IPT_FLAG_COUNTERS = 1
 
 F3 = C.c_float * 3

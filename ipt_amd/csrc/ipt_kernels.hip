@@ -186,8 +186,9 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
     // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
     // (FractalSpheres.cpp:75-84): strict '<' in index order == minimal t,
     // lowest index among equal t, and a sphere never wins a tie with a plane.
-    int p;
-    float best = trace_box_planes_only(o, d, &p);
+    int p = -1;
+    float best = inf_();  // FractalSpheres: no walls
+    if (GEOM == IPT_GEOM_SPHERES_IN_BOX) best = trace_box_planes_only(o, d, &p);
     int bidx = -1;
     if (kp.n_nodes > 0) {
         const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
@@ -243,7 +244,9 @@ constexpr int kLdsCand = 512;
 // sphere-frame builds per workgroup step (overflow lanes retry next step):
 // the box scene makes ~25 per step, the sphere-list scene (nearly every hit a
 // sphere) well over 64
-__host__ __device__ constexpr int frame_slots(int geom) { return geom == IPT_GEOM_SPHERES_IN_BOX ? 256 : 64; }
+__host__ __device__ constexpr int frame_slots(int geom) {
+    return geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES ? 256 : 64;
+}
 // LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
 // task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
 // so unsharded launches do not allocate it).
@@ -694,15 +697,15 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             float li_pow = 0.0f;
             auto light_step = [&](int l) {
                 const LightDev& L = LS.light(l);
-                vec3 hp;
-                const bool h = light_trace(L, ro, rd, &hp);
+                vec3 hp, hn;
+                const bool h = light_trace(L, ro, rd, &hp, &hn);
                 if (IPT_ABL == 4) {
-                    vec3 hq;
-                    const bool h2 = light_trace(L, ro, rd * (1.0f + kp.abl_zero), &hq);
-                    keep_alive(light_pdf(L, ro, h2, hq));
+                    vec3 hq, hm;
+                    const bool h2 = light_trace(L, ro, rd * (1.0f + kp.abl_zero), &hq, &hm);
+                    keep_alive(light_pdf(L, ro, h2, hq, hm));
                 }
                 if (COUNT) ++c_ltest;
-                if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp);
+                if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp, hn);
                 if (h && (!has_li || length(li_pos - ro) > length(hp - ro))) {
                     has_li = true;
                     li_pos = hp;
@@ -993,15 +996,15 @@ __global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ p
             v = frame_cosine_value(make_frame(o), d);
         } else if (kind == 1) {
             const LightDev& L = lights[(int)params[3]];
-            vec3 hp;
-            const bool h = light_trace(L, o, d, &hp);
-            v = light_pdf(L, o, h, hp);
+            vec3 hp, hn;
+            const bool h = light_trace(L, o, d, &hp, &hn);
+            v = light_pdf(L, o, h, hp, hn);
         } else {
             float lmix = 0.0f;
             for (int l = 0; l < nl; ++l) {
-                vec3 hp;
-                const bool h = light_trace(lights[l], o, d, &hp);
-                lmix += weights[l] * light_pdf(lights[l], o, h, hp);
+                vec3 hp, hn;
+                const bool h = light_trace(lights[l], o, d, &hp, &hn);
+                lmix += weights[l] * light_pdf(lights[l], o, h, hp, hn);
             }
             v = lmix + weights[nl] * frame_cosine_value(make_frame(v3(params[3], params[4], params[5])), d);
         }
@@ -1199,6 +1202,7 @@ int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
         case IPT_GEOM_SPHERES_IN_BOX: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES_IN_BOX>(ctx, kp, st);
         case IPT_GEOM_FLOOR: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_FLOOR>(ctx, kp, st);
         case IPT_GEOM_CORNER: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_CORNER>(ctx, kp, st);
+        case IPT_GEOM_SPHERES: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES>(ctx, kp, st);
         default: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
     }
 }
@@ -1391,7 +1395,7 @@ void ipt_destroy(ipt_ctx* ctx) {
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!ctx) return IPT_E_INVALID;
     if (!s) return fail(ctx, IPT_E_INVALID, "scene is NULL");
-    if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_CORNER)
+    if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_SPHERES)
         return fail(ctx, IPT_E_UNSUPPORTED, "unknown geometry_kind");
     if (s->n_lights < 0 || s->n_lights > kMaxLights || (s->n_lights > 0 && !s->lights))
         return fail(ctx, IPT_E_UNSUPPORTED, "n_lights out of range");
@@ -1401,10 +1405,12 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     const int nl = s->n_lights;
     std::vector<LightDev> L(std::max(nl, 1));
     std::vector<float> powers(std::max(nl, 1));
+    bool any_round = false;
     for (int i = 0; i < nl; ++i) {
         const ipt_area_light& a = s->lights[i];
-        if (a.type != IPT_LIGHT_AREA_DIAMOND && a.type != IPT_LIGHT_AREA_TRIANGLE)
+        if (a.type < IPT_LIGHT_AREA_DIAMOND || a.type > IPT_LIGHT_OUTER_SPHERE)
             return fail(ctx, IPT_E_UNSUPPORTED, "unknown light type");
+        if (a.type >= IPT_LIGHT_SPHERE) any_round = true;
         L[i] = make_light(v3(a.position[0], a.position[1], a.position[2]),
                           v3(a.x_axis[0], a.x_axis[1], a.x_axis[2]),
                           v3(a.y_axis[0], a.y_axis[1], a.y_axis[2]), a.power, a.type);
@@ -1441,13 +1447,13 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     std::vector<BvhNode> bnodes;
     std::vector<BvhSphere> bprims;
     int per_order = 0;
-    if (s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX && s->n_spheres > 16)
+    if ((s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX || s->geometry_kind == IPT_GEOM_SPHERES) && s->n_spheres > 16)
         bvh_build_spheres(reinterpret_cast<const float*>(sph.data()), s->n_spheres, cam, B, bnodes, bprims,
                           &per_order);
     // light BVH: only for the global-memory light mode (n_lights > kLdsLights)
     std::vector<BvhNode> lnodes;
     int n_lnodes = 0;
-    if (nl > kLdsLights) {
+    if (nl > kLdsLights && !any_round) {  // the light BVH indexes AreaLights only
         std::vector<std::array<float, 3>> lp(nl), lx(nl), ly(nl);
         std::vector<std::array<float, 9>> li(nl);
         for (int i = 0; i < nl; ++i) {

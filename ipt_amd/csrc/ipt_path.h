@@ -175,8 +175,47 @@ IPT_HD float trace_box(vec3 o, vec3 d, int* prim) {
 IPT_HD bool gt_1em6(float f) { return f > u2f(0x358637bdu); }
 
 // ----------------------------------------------------------------- lights
-// AreaLight::traceRay (lighting.cpp:107-144); returns hit flag, position.
-IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit) {
+// Light types: 0 AreaLight diamond, 1 AreaLight triangle (lighting.cpp:79-144),
+// 2 SphereLight, 3 PointLight, 4 InvertedSphereLight (lighting.h:31-73,
+// lighting.cpp:146-207). Round lights keep the centre in P and the radius in x.x.
+
+// SphereLight's own intersection_with_sphere (lighting.cpp:11-36), in the
+// light's frame (o = origin - centre): float discriminant with dot(d, d), the
+// roots in f64 from sqrtf(desc), rejection below 1e-6, and the front/back sign
+// test. Returns t (inf = miss).
+IPT_HD float round_light_t(float radius, vec3 o, vec3 d) {
+    const float b = dot(o, d);
+    const float dd = dot(d, d);
+    const float desc = 4.0f * (b * b) - 4.0f * dd * (dot(o, o) - radius * radius);
+    if (desc < 0.0f) return inf_();
+    const double sd = (double)sqrt_(desc);
+    float t1 = (float)((-2.0 * (double)b - sd) / 2.0 / (double)dd);
+    float t2 = (float)((-2.0 * (double)b + sd) / 2.0 / (double)dd);
+    if (lt_1em6(t1)) t1 = inf_();
+    if (lt_1em6(t2)) t2 = inf_();
+    const float t = (t2 < t1) ? t2 : t1;  // std::min(t1, t2)
+    const vec3 pos = o + d * t;
+    const vec3 outer_normal = normalize(pos);
+    const float direction_sign = dot(outer_normal, o - pos);
+    const float position_sign = length(o) - radius;
+    if (direction_sign * position_sign <= 0.0f) return inf_();
+    return t;  // inf when both roots were rejected (the NaN sign test passes it through)
+}
+
+// Light::traceRay: hit flag, position and the light's normal there.
+//   AreaLight::traceRay (lighting.cpp:107-144);
+//   SphereLight::traceRay (lighting.cpp:161-173), InvertedSphereLight flips
+//   the normal (lighting.h:61-66), PointLight never hits (lighting.h:39-41).
+IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* nrm) {
+    if (L.type >= 2) {
+        if (L.type == 3) return false;
+        const float t = round_light_t(L.x.x, o - L.P, d);
+        if (t == inf_()) return false;
+        *hit = o + d * t;
+        const vec3 n = normalize(*hit - L.P);
+        *nrm = L.type == 4 ? -n : n;
+        return true;
+    }
     const float n_dir = dot(L.n, d);
     if (lt_1em6(fabs_(n_dir)) || n_dir > 0.0f) return false;
     const float t = div_(dot(L.n, L.P - o), n_dir);
@@ -190,34 +229,63 @@ IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit) {
         h = coord.x >= 0.0f && coord.y >= 0.0f && coord.x + coord.y <= 1.0f;
     if (!h) return false;
     *hit = L.P + rel;
+    *nrm = L.n;
     return true;
 }
 
-// DdfFromLight::value for a direction whose light trace is `has`/`hit`
+// DdfFromLight::value for a direction whose light trace is `has`/`hit`/`nrm`
 // (lighting.cpp:136-148).
-IPT_HD float light_pdf(const LightDev& L, vec3 o, bool has, vec3 hit) {
+IPT_HD float light_pdf(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nrm) {
     if (!has) return 0.0f;
     const vec3 dir = normalize(hit - o);
-    const float cosinus = dot(L.n, -dir);
+    const float cosinus = dot(nrm, -dir);
     if (cosinus < 0.0f) return 0.0f;
     const vec3 ho = hit - o;
     const float decay = dot(ho, ho);
     return div_(div_(decay, cosinus), L.area);
 }
 
-// DdfFromLight::sample via AreaLight::sample (lighting.cpp:125-134, 93-104).
+// DdfFromLight::sample (lighting.cpp:125-134) via Light::sample:
+//   AreaLight::sample (lighting.cpp:93-104);
+//   SphereLight::sample (lighting.cpp:176-193): u1 = 2*randf()-1, acosf,
+//   phi = (float)(2*M_PI*u2), sin/cos of phi fused to sincosf by GCC;
+//   InvertedSphereLight flips the normal; PointLight::sample (lighting.cpp:
+//   196-212): the normal is (sin a cos p, sin a sin p, u1), the point fixed.
 // Returns vec3() when the sampled point faces away (cosinus < 1e-5f).
 IPT_HD vec3 light_sample_dir(const LightDev& L, vec3 o, float u1, float u2raw) {
-    const float u2 = u2raw * (L.type == 1 ? 1.0f - u1 : 1.0f);
-    const vec3 pos = (L.x * u1 + L.y * u2) + L.P;
+    vec3 pos, nrm;
+    if (L.type >= 2) {
+        const float uc = u1 * 2.0f - 1.0f;
+        const float alpha = acosf_(uc);
+        const float phi = two_pi_times(u2raw);
+        float sp, cp;
+        sincosf_small_(phi, &sp, &cp);
+        if (L.type == 3) {
+            const float r = sinf_small_(alpha);
+            nrm = v3(r * cp, r * sp, uc);
+            pos = L.P;
+        } else {
+            const float r = L.x.x * sinf_small_(alpha);
+            const vec3 q = v3(r * cp, r * sp, L.x.x * uc);
+            pos = q + L.P;
+            nrm = normalize(q);
+            if (L.type == 4) nrm = -nrm;
+        }
+    } else {
+        const float u2 = u2raw * (L.type == 1 ? 1.0f - u1 : 1.0f);
+        pos = (L.x * u1 + L.y * u2) + L.P;
+        nrm = L.n;
+    }
     const vec3 dir = normalize(pos - o);
-    const float cosinus = dot(L.n, -dir);
+    const float cosinus = dot(nrm, -dir);
     if (cosinus < 1e-5f) return v3(0.0f, 0.0f, 0.0f);
     return dir;
 }
 
-// AreaLight constructor derived fields (lighting.cpp:79-90) + the per-call
-// normal/power expressions of traceRay/sample.
+// Light constructor derived fields: AreaLight (lighting.cpp:79-90) + the
+// per-call normal/power expressions of traceRay/sample; SphereLight /
+// InvertedSphereLight: area = 4.0*M_PI*radius*radius in f64 (lighting.h:
+// 46-52); PointLight: area 0 (lighting.h:33-37).
 IPT_HD LightDev make_light(vec3 P, vec3 x, vec3 y, float power, int type) {
     LightDev L;
     L.P = P;
@@ -225,6 +293,14 @@ IPT_HD LightDev make_light(vec3 P, vec3 x, vec3 y, float power, int type) {
     L.y = y;
     L.type = type;
     L.pad = 0;
+    if (type >= 2) {
+        const double r = (double)x.x;
+        L.area = type == 3 ? 0.0f : (float)(4.0 * u2d(0x400921fb54442d18ull) * r * r);
+        L.n = v3(0.0f, 0.0f, 0.0f);
+        for (int c = 0; c < 3; ++c) L.inv.c[c] = v3(0.0f, 0.0f, 0.0f);
+        L.spow = power / L.area;
+        return L;
+    }
     const float full_area = length(cross(x, y));
     L.area = type == 0 ? full_area : full_area / 2.0f;
     mat3 m;

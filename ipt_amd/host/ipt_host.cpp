@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 
 #include "../csrc/ipt_math.h"  // glm-order float arithmetic (vec3, cross, normalize)
 
@@ -63,9 +64,57 @@ void CollectionLighting::addSquareLight(vec3f corner, vec3f normal, vec3f x_side
 void CollectionLighting::addTriangleLight(vec3f corner, vec3f x_side, vec3f y_side, float power) {
     lights.push_back(std::make_shared<const AreaLight>(corner, x_side, y_side, power, AreaLight::TYPE_TRIANLE));
 }
-void CollectionLighting::addPointLight(vec3f, float, float) { unsupported("PointLight"); }
-void CollectionLighting::addSphereLight(vec3f, float, float) { unsupported("SphereLight"); }
-void CollectionLighting::addOuterLight(float, float) { unsupported("InvertedSphereLight (addOuterLight)"); }
+SphereLight::SphereLight(vec3f origin, float r, float p) : position(origin), radius(r) { power = p; }
+PointLight::PointLight(vec3f origin, float vr, float p) : position(origin), virtual_radius(vr) { power = p; }
+InvertedSphereLight::InvertedSphereLight(vec3f origin, float r, float p) : SphereLight(origin, r, p) {}
+
+// CollectionLighting.cpp:36-55
+void CollectionLighting::addPointLight(vec3f position, float virtual_radius, float power) {
+    lights.push_back(std::make_shared<const PointLight>(position, virtual_radius, power));
+}
+void CollectionLighting::addSphereLight(vec3f position, float radius, float power) {
+    lights.push_back(std::make_shared<const SphereLight>(position, radius, power));
+}
+void CollectionLighting::addOuterLight(float radius, float power) {
+    lights.push_back(std::make_shared<const InvertedSphereLight>(vec3f{0, 0, 0}, radius, power));
+}
+
+// FractalSpheres.cpp:16-44 (generate_spheres) and 46-67 (the constructor),
+// float arithmetic with glibc asinf/sinf as the reference's build calls them.
+namespace {
+void generate_spheres(float r1, vec3 c1, float r2, vec3 c2, bool light_from_left,
+                      const std::function<bool(float, vec3)>& callback) {
+    const float L = length(c1 - c2) - r1 - r2;
+    if (L < 0.01) return;
+    const float sin_alpha = r1 / (r1 + L);
+    const float alpha = std::asin(sin_alpha);
+    const float sin_beta = r2 / (r2 + L);
+    const float beta = std::asin(sin_beta);
+    const float pi = 3.14159265358979323846f;  // M_PIf32
+    const float gamma = pi - alpha - beta;
+    const float A = L * sin_alpha / std::sin(gamma);
+    const float x = A * std::sin(gamma / 2) / std::sin(pi - beta - gamma / 2);
+    const vec3 c3 = c1 + normalize(c2 - c1) * (x + r1);
+    const float r3 = x * sin_beta;
+    if (callback(r3, c3)) return;
+    if (light_from_left)
+        generate_spheres(r1, c1, r3, c3, !light_from_left, callback);
+    else
+        generate_spheres(r3, c3, r2, c2, !light_from_left, callback);
+}
+}  // namespace
+
+FractalSpheres::FractalSpheres() {
+    auto add_sphere = [this](float r, vec3 c) -> bool {
+        if (r < 0.001) return true;
+        rs.push_back(r);
+        cs.push_back(h(c));
+        return false;
+    };
+    add_sphere(0.5f, v3(-2, 0, 0));
+    add_sphere(0.5f, v3(2, 0, 0));
+    generate_spheres(0.5f, v3(-2, 0, 0), 0.5f, v3(2, 0, 0), true, add_sphere);
+}
 
 SimpleCamera::SimpleCamera(vec3f pos, vec3f dir, vec3f up_hint) : position(pos), direction(dir) {
     const vec3 r = normalize(cross(g(dir), g(up_hint)));
@@ -160,7 +209,12 @@ Scene make_scene_lit_corner() {
                  std::make_shared<SimpleCamera>(h(camera_pos), h(camera_dir))};
 }
 
-Scene make_scene_fractal() { unsupported("make_scene_fractal (FractalSpheres + SphereLight)"); }
+Scene make_scene_fractal() {
+    auto lighting = std::make_shared<CollectionLighting>();
+    lighting->addSphereLight(vec3f{-5.5f, 0, 0}, 1);
+    auto camera = std::make_shared<SimpleCamera>(vec3f{0.0f, -4.0f, 0.0f}, vec3f{0, 1, 0});
+    return Scene{std::make_shared<FractalSpheres>(), lighting, camera};
+}
 Scene make_scene_smallpt() { unsupported("make_scene_smallpt (GeometrySmallPt)"); }
 
 Scene make_scene_by_name(const std::string& spec) {
@@ -178,6 +232,8 @@ Scene make_scene_by_name(const std::string& spec) {
     if (n == "spheres") return make_scene_spheres((int)num(1, 10000), (uint64_t)num(2, 1));
     if (n == "random_lights") return make_scene_random_lights((int)num(1, 64), (uint64_t)num(2, 7));
     if (n == "fractal") return make_scene_fractal();
+    if (n == "square_lit_by_square" || n == "floor") return make_scene_square_lit_by_square();
+    if (n == "lit_corner" || n == "corner") return make_scene_lit_corner();
     if (n == "smallpt") return make_scene_smallpt();
     if (n == "square_lit_by_square") return make_scene_square_lit_by_square();
     if (n == "lit_corner") return make_scene_lit_corner();
@@ -194,6 +250,16 @@ FlatScene flatten(const Scene& s) {
         out.scene.geometry_kind = IPT_GEOM_FLOOR;
     } else if (dynamic_cast<const GeometryCorner*>(s.geometry.get())) {
         out.scene.geometry_kind = IPT_GEOM_CORNER;
+    } else if (auto fs = dynamic_cast<const FractalSpheres*>(s.geometry.get())) {
+        out.scene.geometry_kind = IPT_GEOM_SPHERES;
+        for (size_t i = 0; i < fs->rs.size(); ++i) {
+            ipt_sphere t{};
+            t.center[0] = fs->cs[i].x;
+            t.center[1] = fs->cs[i].y;
+            t.center[2] = fs->cs[i].z;
+            t.radius = fs->rs[i];
+            out.spheres.push_back(t);
+        }
     } else if (auto sp = dynamic_cast<const SpheresInBox*>(s.geometry.get())) {
         out.scene.geometry_kind = IPT_GEOM_SPHERES_IN_BOX;
         for (const auto& q : sp->spheres) {
@@ -210,9 +276,28 @@ FlatScene flatten(const Scene& s) {
     auto coll = dynamic_cast<const CollectionLighting*>(s.lighting.get());
     if (!coll) unsupported("lighting type");
     for (const auto& l : coll->lights) {
+        ipt_area_light L{};
+        L.power = l->power;
+        if (auto sl = dynamic_cast<const SphereLight*>(l.get())) {
+            L.position[0] = sl->position.x;
+            L.position[1] = sl->position.y;
+            L.position[2] = sl->position.z;
+            L.x_axis[0] = sl->radius;
+            L.type = dynamic_cast<const InvertedSphereLight*>(l.get()) ? IPT_LIGHT_OUTER_SPHERE : IPT_LIGHT_SPHERE;
+            out.lights.push_back(L);
+            continue;
+        }
+        if (auto pl = dynamic_cast<const PointLight*>(l.get())) {
+            L.position[0] = pl->position.x;
+            L.position[1] = pl->position.y;
+            L.position[2] = pl->position.z;
+            L.x_axis[0] = pl->virtual_radius;
+            L.type = IPT_LIGHT_POINT;
+            out.lights.push_back(L);
+            continue;
+        }
         auto a = dynamic_cast<const AreaLight*>(l.get());
         if (!a) unsupported("light type");
-        ipt_area_light L{};
         const vec3f* src[3] = {&a->position, &a->x_axis, &a->y_axis};
         float* dst[3] = {L.position, L.x_axis, L.y_axis};
         for (int k = 0; k < 3; ++k) {

@@ -16,9 +16,8 @@
 // Objects here are scene DESCRIPTIONS: nothing in this layer traces a ray on
 // the CPU. Rendering is GpuRenderer / render_samples_gpu, i.e. ipt_render on
 // a gfx950 GPU, and it throws IptError(IPT_E_DEVICE) when there is none.
-// Scene types the GPU kernels do not implement yet (§8(f) row 1: point,
-// sphere and outer lights, the fractal / smallpt scenes) throw
-// IptError(IPT_E_UNSUPPORTED) where they are created.
+// Scene types the GPU kernels do not implement yet (§8(f) row 1: the
+// smallpt scene) throw IptError(IPT_E_UNSUPPORTED) where they are created.
 #pragma once
 
 #include <cstddef>
@@ -63,6 +62,13 @@ struct SpheresInBox : Geometry {
 struct GeometryFloor : Geometry {};
 // The x = -1, y = -1, z = -1 faces (GeometryCorner.cpp:10-42).
 struct GeometryCorner : Geometry {};
+// FractalSpheres (FractalSpheres.cpp:46-97): the generated sphere chain
+// between two r=0.5 spheres at (-2,0,0) and (2,0,0), no walls.
+struct FractalSpheres : Geometry {
+    std::vector<float> rs;
+    std::vector<vec3f> cs;
+    FractalSpheres();
+};
 
 // ------------------------------------------------------------- lighting
 struct Light {
@@ -77,6 +83,23 @@ struct AreaLight : Light {
     AreaLight(vec3f corner, vec3f x_axis, vec3f y_axis, float power, type_t type = TYPE_DIAMOND);
 };
 
+// SphereLight(origin, radius, power=1) (lighting.h:44-54)
+struct SphereLight : Light {
+    vec3f position;
+    float radius;
+    SphereLight(vec3f origin, float radius, float power = 1.0f);
+};
+// PointLight(origin, virtual_radius, power=1) (lighting.h:31-42)
+struct PointLight : Light {
+    vec3f position;
+    float virtual_radius;
+    PointLight(vec3f origin, float virtual_radius, float power = 1.0f);
+};
+// InvertedSphereLight(origin, radius, power) (lighting.h:57-72)
+struct InvertedSphereLight : SphereLight {
+    InvertedSphereLight(vec3f origin, float radius, float power);
+};
+
 struct Lighting {
     virtual ~Lighting() = default;
 };
@@ -85,10 +108,9 @@ struct CollectionLighting : Lighting {
     // y_side = cross(normal, x_side) (CollectionLighting.cpp:42-46)
     void addSquareLight(vec3f corner, vec3f normal, vec3f x_side, float power = 1.0f);
     void addTriangleLight(vec3f corner, vec3f x_side, vec3f y_side, float power = 1.0f);
-    // Not on the GPU path yet (§8(f) row 1): throw IptError(IPT_E_UNSUPPORTED).
     void addPointLight(vec3f position, float virtual_radius, float power = 1.0f);
     void addSphereLight(vec3f position, float radius, float power = 1.0f);
-    void addOuterLight(float radius, float power = 1.0f);
+    void addOuterLight(float radius, float power = 1.0f);  // InvertedSphereLight at the origin
 };
 
 // --------------------------------------------------------------- camera
@@ -128,8 +150,8 @@ Scene make_scene_spheres(int n, uint64_t seed = 1);       // box + n spheres (C3
 Scene make_scene_random_lights(int n, uint64_t seed = 7);  // overlapping random emitters (tests)
 Scene make_scene_square_lit_by_square();                  // sample_scenes.cpp:73-85
 Scene make_scene_lit_corner();                            // sample_scenes.cpp:88-108
-// not on the GPU path yet (§8(f) row 1): throw IptError(IPT_E_UNSUPPORTED)
-Scene make_scene_fractal();
+Scene make_scene_fractal();                               // sample_scenes.cpp:43-55
+// not on the GPU path yet (§8(f) row 1): throws IptError(IPT_E_UNSUPPORTED)
 Scene make_scene_smallpt();
 // "box", "box_lights:K", "spheres:N[:SEED]", "random_lights:N[:SEED]", "fractal", ...
 Scene make_scene_by_name(const std::string& name);

@@ -14,8 +14,9 @@ from __future__ import annotations
 
 import numpy as np
 
-from .capi import (IPT_GEOM_CORNER, IPT_GEOM_FLOOR, IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES_IN_BOX,
-                   IPT_LIGHT_AREA_DIAMOND, IPT_LIGHT_AREA_TRIANGLE)
+from .capi import (IPT_GEOM_CORNER, IPT_GEOM_FLOOR, IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES,
+                   IPT_GEOM_SPHERES_IN_BOX, IPT_LIGHT_AREA_DIAMOND, IPT_LIGHT_AREA_TRIANGLE, IPT_LIGHT_OUTER_SPHERE,
+                   IPT_LIGHT_POINT, IPT_LIGHT_SPHERE)
 
 f32 = np.float32
 
@@ -102,6 +103,92 @@ def make_scene_lit_corner():
     camera_dir = normalize((_v(0.0, 0.0, 0.0) - camera_pos).astype(f32))
     return {"geometry_kind": IPT_GEOM_CORNER, "lights": [light], "spheres": [],
             "camera": simple_camera(camera_pos, camera_dir)}
+
+
+def sphere_light(position, radius, power=1.0):
+    """CollectionLighting::addSphereLight (CollectionLighting.cpp:39-41)."""
+    return {"position": _v(*position).tolist(), "x_axis": [float(f32(radius)), 0.0, 0.0],
+            "y_axis": [0.0, 0.0, 0.0], "power": float(f32(power)), "type": IPT_LIGHT_SPHERE}
+
+
+def point_light(position, virtual_radius, power=1.0):
+    """CollectionLighting::addPointLight (CollectionLighting.cpp:36-38)."""
+    return {"position": _v(*position).tolist(), "x_axis": [float(f32(virtual_radius)), 0.0, 0.0],
+            "y_axis": [0.0, 0.0, 0.0], "power": float(f32(power)), "type": IPT_LIGHT_POINT}
+
+
+def outer_light(radius, power=1.0):
+    """CollectionLighting::addOuterLight (CollectionLighting.cpp:52-55)."""
+    return {"position": [0.0, 0.0, 0.0], "x_axis": [float(f32(radius)), 0.0, 0.0],
+            "y_axis": [0.0, 0.0, 0.0], "power": float(f32(power)), "type": IPT_LIGHT_OUTER_SPHERE}
+
+
+_libm = None
+
+
+def _glibc():
+    """glibc's float asinf/sinf, as FractalSpheres' generator calls them."""
+    global _libm
+    if _libm is None:
+        import ctypes
+        _libm = ctypes.CDLL("libm.so.6")
+        for fn in ("asinf", "sinf"):
+            getattr(_libm, fn).restype = ctypes.c_float
+            getattr(_libm, fn).argtypes = [ctypes.c_float]
+    return _libm
+
+
+def fractal_spheres():
+    """FractalSpheres::FractalSpheres (FractalSpheres.cpp:46-67) with
+    generate_spheres (FractalSpheres.cpp:16-44), float arithmetic and glibc
+    asinf/sinf: a list of (centre, radius)."""
+    m = _glibc()
+    pi = f32(3.14159265358979323846)  # M_PIf32
+
+    def length(v):
+        return np.sqrt(dot(v, v), dtype=f32)
+
+    spheres = []
+
+    def add(r, c):
+        if float(r) < 0.001:
+            return True
+        spheres.append((c.astype(f32).tolist(), float(r)))
+        return False
+
+    def gen(r1, c1, r2, c2, left):
+        L = f32(f32(length((c1 - c2).astype(f32)) - r1) - r2)
+        if float(L) < 0.01:
+            return
+        sin_alpha = f32(r1 / f32(r1 + L))
+        alpha = f32(m.asinf(sin_alpha))
+        sin_beta = f32(r2 / f32(r2 + L))
+        beta = f32(m.asinf(sin_beta))
+        gamma = f32(f32(pi - alpha) - beta)
+        A = f32(f32(L * sin_alpha) / f32(m.sinf(gamma)))
+        x = f32(f32(A * f32(m.sinf(f32(gamma / f32(2))))) / f32(m.sinf(f32(f32(pi - beta) - f32(gamma / f32(2))))))
+        c3 = (c1 + (normalize((c2 - c1).astype(f32)) * f32(x + r1)).astype(f32)).astype(f32)
+        r3 = f32(x * sin_beta)
+        if add(r3, c3):
+            return
+        if left:
+            gen(r1, c1, r3, c3, not left)
+        else:
+            gen(r3, c3, r2, c2, not left)
+
+    r1, c1, r2, c2 = f32(0.5), _v(-2.0, 0.0, 0.0), f32(0.5), _v(2.0, 0.0, 0.0)
+    add(r1, c1)
+    add(r2, c2)
+    gen(r1, c1, r2, c2, True)
+    return spheres
+
+
+def make_scene_fractal():
+    """sample_scenes.cpp:43-55: FractalSpheres lit by a unit SphereLight at
+    (-5.5,0,0), camera at (0,-4,0) looking along +y."""
+    cam = simple_camera(_v(0.0, -4.0, 0.0), _v(0.0, 1.0, 0.0))
+    return {"geometry_kind": IPT_GEOM_SPHERES, "lights": [sphere_light((-5.5, 0.0, 0.0), 1.0)],
+            "spheres": fractal_spheres(), "camera": cam}
 
 
 def make_scene_box_lights(k: int = 16):

@@ -167,13 +167,20 @@ struct AreaLightO {
     M3 inverse_matrix;
     float power, area;
     int type;
-    // lighting.cpp:79-90
+    // lighting.cpp:79-90 (AreaLight); types 2-4: SphereLight, PointLight,
+    // InvertedSphereLight (lighting.h:31-73), radius in xa.x
+    float radius = 0.0f;
     AreaLightO(V3 origin, V3 xa, V3 ya, float pw, int ty) {
         position = origin;
         x_axis = xa;
         y_axis = ya;
         power = pw;
         type = ty;
+        if (type >= 2) {
+            radius = xa.x;
+            area = type == 3 ? 0.0f : 4.0 * M_PI * radius * radius;  // lighting.h:50
+            return;
+        }
         float full_area = length(cross(x_axis, y_axis));
         area = type == 0 ? full_area : full_area / 2.0f;
         M3 m;
@@ -183,8 +190,50 @@ struct AreaLightO {
         m.m[2][0] = c.x; m.m[2][1] = c.y; m.m[2][2] = c.z;
         inverse_matrix = inverse(m);
     }
+    // lighting.cpp:176-212 (SphereLight / PointLight ::sample), normal flipped
+    // for InvertedSphereLight (lighting.h:67-71)
+    void sample_round(V3* pos_out, V3* normal_out, float* sp) const {
+        float u1 = randf() * 2.0f - 1.0f;
+        float u2 = randf();
+        float alpha = std::acos(u1);
+        float phi = 2 * M_PI * u2;
+        if (type == 3) {
+            float r = std::sin(alpha);
+            *normal_out = mk(r * std::cos(phi), r * std::sin(phi), u1);
+            *pos_out = position;
+            *sp = std::numeric_limits<float>::signaling_NaN();
+            return;
+        }
+        float r = radius * std::sin(alpha);
+        V3 pos = mk(r * std::cos(phi), r * std::sin(phi), radius * u1);
+        *pos_out = pos + position;
+        *normal_out = normalize(pos);
+        if (type == 4) *normal_out = -*normal_out;
+        *sp = power / area;
+    }
+    // lighting.cpp:11-36: SphereLight's own sphere intersection
+    static float round_t(float radius, V3 origin, V3 direction) {
+        float desc = 4.0f * (dot(origin, direction) * dot(origin, direction)) -
+                     4.0f * dot(direction, direction) * (dot(origin, origin) - radius * radius);
+        if (desc < 0.0f) return INF;
+        float t1 = (-2.0 * dot(origin, direction) - std::sqrt(desc)) / 2.0 / dot(direction, direction);
+        float t2 = (-2.0 * dot(origin, direction) + std::sqrt(desc)) / 2.0 / dot(direction, direction);
+        if (t1 < 1e-6) t1 = INF;
+        if (t2 < 1e-6) t2 = INF;
+        float t = std::min(t1, t2);
+        V3 pos = origin + direction * t;
+        V3 outer_normal = normalize(pos);
+        float direction_sign = dot(outer_normal, origin - pos);
+        float position_sign = length(origin) - radius;
+        if (direction_sign * position_sign <= 0.0f) return INF;
+        return t;
+    }
     // lighting.cpp:93-104
     void sample(V3* pos_out, V3* normal_out, float* sp) const {
+        if (type >= 2) {
+            sample_round(pos_out, normal_out, sp);
+            return;
+        }
         float u1 = randf();
         float u2 = randf() * (type == 1 ? 1.0f - u1 : 1.0f);
         V3 pos = x_axis * u1 + y_axis * u2;
@@ -195,6 +244,16 @@ struct AreaLightO {
     // lighting.cpp:107-144
     bool traceRay(V3 origin, V3 direction, V3* pos_out, V3* normal_out, float* sp) const {
         if (g_cnt) ++g_cnt->ltraces;
+        if (type == 3) return false;  // PointLight::traceRay (lighting.h:39-41)
+        if (type >= 2) {              // SphereLight::traceRay (lighting.cpp:161-173)
+            float t = round_t(radius, origin - position, direction);
+            if (t == INF) return false;
+            *pos_out = origin + direction * t;
+            *normal_out = normalize(*pos_out - position);
+            if (type == 4) *normal_out = -*normal_out;  // InvertedSphereLight (lighting.h:61-66)
+            *sp = power / area;
+            return true;
+        }
         V3 n = normalize(cross(x_axis, y_axis));
         float n_dir = dot(n, direction);
         if (std::abs(n_dir) < 1e-6 || n_dir > 0.0f) return false;
@@ -333,6 +392,10 @@ bool geometry_trace(const SceneO& sc, V3 origin, V3 direction, SurfHit* out) {
         }
     }
     V3 sc_center = mk(0, 0, 0);
+    if (sc.geometry_kind == IPT_GEOM_SPHERES) {  // FractalSpheres: the list alone
+        dist = INF;
+        intersected_plane = -1;
+    }
     if (sc.geometry_kind == IPT_GEOM_SPHERE_IN_BOX) {
         float t = intersection_with_sphere(0.5f, origin, direction);
         if (t < dist) {

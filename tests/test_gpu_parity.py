@@ -199,6 +199,37 @@ def test_sample_scenes_floor_corner_bit_exact(gpu_ctx, oracle, name, n_rays, dep
     assert (ov > 0).mean() > 0.05  # the scene is lit
 
 
+@pytest.mark.parametrize("n_rays,depth_max", [(16, 8), (4, 6)])
+def test_sample_scene_fractal_bit_exact(gpu_ctx, oracle, n_rays, depth_max):
+    """sample_scenes.cpp:43-55: FractalSpheres (sphere list, no walls) lit by a
+    SphereLight (its own intersection and sampler, lighting.cpp:11-36,146-193)."""
+    desc = scenes.make_scene_fractal()
+    p = capi.make_params(48, 40, 2, n_rays=n_rays, depth_max=depth_max)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+    assert (ov > 0).any()  # the sphere light reaches the camera
+
+
+@pytest.mark.parametrize("geom", ["box", "fractal"])
+def test_round_lights_bit_exact(gpu_ctx, oracle, geom):
+    """Sphere, point and inverted-sphere (outer) lights mixed with area lights:
+    CollectionLighting's nearest rule, UnionDdf over all of them, the point
+    light never hit (lighting.h:31-73)."""
+    base = scenes.make_scene_box() if geom == "box" else scenes.make_scene_fractal()
+    desc = dict(base)
+    desc["lights"] = list(base["lights"]) + [
+        scenes.sphere_light((0.3, 0.2, 0.4), 0.15, 0.7),
+        scenes.point_light((-0.4, 0.3, -0.2), 0.05, 0.5),
+        scenes.outer_light(9.0, 0.05),
+        scenes.sphere_light((-0.5, -0.6, 0.5), 0.2, 1.3),
+    ]
+    p = capi.make_params(40, 32, 2, n_rays=8, depth_max=6)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
 def test_spheres_in_box_c3_scene(gpu_ctx, oracle):
     """The full 10k-sphere scene of BASELINE configs[2] (bench C3): BVH walk
     (octant orders, open-floor rays with best = inf) against the oracle's scan."""

@@ -54,13 +54,14 @@ def _py_flat(desc):
     ("random_lights:17:7", lambda: scenes.make_scene_random_lights(17, 7)),
     ("square_lit_by_square", scenes.make_scene_square_lit_by_square),
     ("lit_corner", scenes.make_scene_lit_corner),
+    ("fractal", scenes.make_scene_fractal),
 ])
 def test_cpp_scenes_match_python(dump, name, desc_fn):
     out = subprocess.run([str(dump), "scene", name], check=True, capture_output=True, text=True).stdout
     assert json.loads(out) == _py_flat(desc_fn())
 
 
-@pytest.mark.parametrize("name", ["fractal", "smallpt"])
+@pytest.mark.parametrize("name", ["smallpt"])
 def test_unsupported_scenes_fail_loudly(dump, name):
     out = subprocess.run([str(dump), "scene-error", name], check=True, capture_output=True, text=True).stdout
     assert int(out) == capi.IPT_E_UNSUPPORTED

@@ -197,10 +197,12 @@ def _ref_scenes():
     return out
 
 
-@pytest.mark.parametrize("idx,name", [(0, "make_scene_square_lit_by_square"), (1, "make_scene_lit_corner")])
+@pytest.mark.parametrize("idx,name", [(0, "make_scene_square_lit_by_square"), (1, "make_scene_lit_corner"),
+                                      (2, "make_scene_fractal")])
 def test_area_light_scenes_flattening(lib, idx, name):
-    """ipt_amd.scenes reproduces sample_scenes.cpp's floor and corner scenes:
-    camera fields, light fields and the light's own traceRay on probes."""
+    """ipt_amd.scenes reproduces sample_scenes.cpp's floor, corner and fractal
+    scenes: camera fields, light fields (AreaLight, triangle AreaLight,
+    SphereLight) and the light's own traceRay on probes."""
     from ipt_amd import scenes
 
     cam_ref, lights_ref, probes = _ref_scenes()[idx]
@@ -224,3 +226,13 @@ def test_area_light_scenes_flattening(lib, idx, name):
             n_hit += 1
             assert np.array_equal(bits(out), bits(r[7:11]))
     assert n_hit > 20
+
+
+def test_fractal_spheres_generator():
+    """ipt_amd.scenes.fractal_spheres() == the reference's generate_spheres
+    driven as FractalSpheres' constructor does (ref_fractal_spheres.bin)."""
+    from ipt_amd import scenes
+
+    R = np.fromfile(GOLD / "ref_fractal_spheres.bin", dtype=np.float32)
+    mine = np.array([v for c, r in scenes.fractal_spheres() for v in (*c, r)], np.float32)
+    assert int(R[0]) == len(mine) // 4 and np.array_equal(bits(mine), bits(R[1:]))
