@@ -261,7 +261,9 @@ __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
 // Where the lights live during the step loop (compile time, so that no
 // generic/flat pointer is ever formed: a flat load would make the compiler
 // wait for every outstanding radiance store).
-enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3 };
+enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3, kLightsAny = 4 };
+// kLightsAny: global-memory lights of any type (sphere, point, outer lights
+// present); the other modes are AreaLight-only.
 
 template <int LMODE>
 struct LightSet {
@@ -276,7 +278,7 @@ struct LightSet {
     __device__ __forceinline__ const LightDev& light(int i) const {
         if (LMODE == kLightsOne) return one;
         if (LMODE == kLightsLds) return lds[i];
-        return glob[i];
+        return glob[i];  // kLightsGlobal, kLightsAny
     }
     __device__ __forceinline__ float weight(int i) const {
         if (LMODE == kLightsOne) return w0;
@@ -568,7 +570,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             int c = 0;
             if (LMODE == kLightsOne) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
-            } else if (LMODE == kLightsGlobal && kp.cdf_bsearch) {
+            } else if ((LMODE == kLightsGlobal || LMODE == kLightsAny) && kp.cdf_bsearch) {
                 // first c with r < cdf[c] (else nl+1): the scan's answer on a
                 // non-decreasing cdf (checked at upload)
                 int hi = nl + 1;
@@ -665,8 +667,9 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             vec3 dir = v3(0, 0, 0);
             if (pick < nl) {
                 IPT_PHASE(7);
-                dir = light_sample_dir(LS.light(pick), tpos, u1, u2);
-                if (IPT_ABL == 7) keep_alive(light_sample_dir(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
+                dir = light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1, u2);
+                if (IPT_ABL == 7)
+                    keep_alive(light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
                 if (COUNT) ++c_lsamp;
             } else if (pick == nl) {
                 dir = frame_apply(tfr, v3(xcos[0 * kBlock + slot_c], xcos[1 * kBlock + slot_c],
@@ -698,10 +701,10 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             auto light_step = [&](int l) {
                 const LightDev& L = LS.light(l);
                 vec3 hp, hn;
-                const bool h = light_trace(L, ro, rd, &hp, &hn);
+                const bool h = light_trace<LMODE == kLightsAny>(L, ro, rd, &hp, &hn);
                 if (IPT_ABL == 4) {
                     vec3 hq, hm;
-                    const bool h2 = light_trace(L, ro, rd * (1.0f + kp.abl_zero), &hq, &hm);
+                    const bool h2 = light_trace<LMODE == kLightsAny>(L, ro, rd * (1.0f + kp.abl_zero), &hq, &hm);
                     keep_alive(light_pdf(L, ro, h2, hq, hm));
                 }
                 if (COUNT) ++c_ltest;
@@ -1063,6 +1066,7 @@ struct ipt_ctx {
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
+    bool any_round_light = false;
     int bpc_override = 0;
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     // work buffers
@@ -1208,6 +1212,7 @@ int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
 }
 template <int MAXSUSP, bool COUNT>
 int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
+    if (ctx->any_round_light) return launch_path3<MAXSUSP, COUNT, kLightsAny>(ctx, kp, st);
     if (kp.n_lights == 1) return launch_path3<MAXSUSP, COUNT, kLightsOne>(ctx, kp, st);
     if (kp.n_lights <= kLdsLights) return launch_path3<MAXSUSP, COUNT, kLightsLds>(ctx, kp, st);
     return launch_path3<MAXSUSP, COUNT, kLightsGlobal>(ctx, kp, st);
@@ -1496,6 +1501,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         ctx->n_light_nodes = n_lnodes;
     }
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
+    ctx->any_round_light = any_round;
     if (!bnodes.empty()) {
         HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_nodes, sizeof(BvhNode) * bnodes.size()));
         HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_prims, sizeof(BvhSphere) * bprims.size()));
