@@ -57,7 +57,12 @@ enum {
     /* FractalSpheres (FractalSpheres.cpp:69-97): the sphere list alone, no
        walls, with the same acceptance rule as IPT_GEOM_SPHERES_IN_BOX.
        sample_scenes' make_scene_fractal. */
-    IPT_GEOM_SPHERES = 4
+    IPT_GEOM_SPHERES = 4,
+    /* GeometrySmallPt (GeometrySmallPt.cpp:11-58): the sphere list (smallpt's
+       room: pass its 7 spheres) intersected in double precision
+       (Sphere::intersect, eps 1e-4), strict-< nearest, normal flipped for
+       radius >= 100. sample_scenes' make_scene_smallpt. */
+    IPT_GEOM_SMALLPT = 5
 };
 
 /* Light kinds (reference src/lighting/lighting.h). Round lights use the

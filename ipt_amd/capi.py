@@ -29,6 +29,7 @@ IPT_GEOM_SPHERES_IN_BOX = 1
 IPT_GEOM_FLOOR = 2
 IPT_GEOM_CORNER = 3
 IPT_GEOM_SPHERES = 4
+IPT_GEOM_SMALLPT = 5
 IPT_LIGHT_AREA_DIAMOND = 0
 IPT_LIGHT_AREA_TRIANGLE = 1
 IPT_LIGHT_SPHERE, IPT_LIGHT_POINT, IPT_LIGHT_OUTER_SPHERE = 2, 3, 4

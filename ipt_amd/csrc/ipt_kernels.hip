@@ -183,6 +183,33 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
         *prim = t == inf_() ? -1 : p;
         return t;
     }
+    if (GEOM == IPT_GEOM_SMALLPT) {  // GeometrySmallPt.cpp:14-47, double precision
+        double min_t = (double)inf_();
+        int mi = -1;
+        for (int i = 0; i < kp.n_spheres; ++i) {
+            const float4 sp = kp.spheres[i];
+            const vec3 op = v3(sp.x, sp.y, sp.z) - o;  // p - ro (float)
+            const double rad = (double)sp.w;
+            const double b = (double)dot(op, d);
+            double det = b * b - (double)dot(op, op) + rad * rad;
+            double t = 0.0;
+            if (!(det < 0.0)) {
+                det = sqrtd_(det);
+                t = b - det;
+                if (!(t > 1e-4)) {
+                    t = b + det;
+                    if (!(t > 1e-4)) t = 0.0;
+                }
+            }
+            if (COUNT) ++c_tests;
+            if (t != 0.0 && t < min_t) {
+                min_t = t;
+                mi = i;
+            }
+        }
+        *prim = mi >= 0 ? 6 + mi : -1;
+        return mi >= 0 ? (float)min_t : inf_();
+    }
     // planes as GeometrySphereInBox, then spheres with FractalSpheres' rule
     // (FractalSpheres.cpp:75-84): strict '<' in index order == minimal t,
     // lowest index among equal t, and a sphere never wins a tie with a plane.
@@ -245,7 +272,7 @@ constexpr int kLdsCand = 512;
 // the box scene makes ~25 per step, the sphere-list scene (nearly every hit a
 // sphere) well over 64
 __host__ __device__ constexpr int frame_slots(int geom) {
-    return geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES ? 256 : 64;
+    return geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES || geom == IPT_GEOM_SMALLPT ? 256 : 64;
 }
 // LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
 // task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
@@ -539,6 +566,9 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             } else {
                 const float4 sp = kp.spheres[tkind - 6];
                 nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
+                // GeometrySmallPt.cpp:41: -normalize(v) for the room spheres;
+                // normalize(-v) is the same bits (negation is exact)
+                if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
             }
             xfr[0 * kFrameSlots + slot_f] = nrm.x;
             xfr[1 * kFrameSlots + slot_f] = nrm.y;
@@ -1207,6 +1237,7 @@ int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
         case IPT_GEOM_FLOOR: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_FLOOR>(ctx, kp, st);
         case IPT_GEOM_CORNER: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_CORNER>(ctx, kp, st);
         case IPT_GEOM_SPHERES: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES>(ctx, kp, st);
+        case IPT_GEOM_SMALLPT: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SMALLPT>(ctx, kp, st);
         default: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
     }
 }
@@ -1400,7 +1431,7 @@ void ipt_destroy(ipt_ctx* ctx) {
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!ctx) return IPT_E_INVALID;
     if (!s) return fail(ctx, IPT_E_INVALID, "scene is NULL");
-    if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_SPHERES)
+    if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_SMALLPT)
         return fail(ctx, IPT_E_UNSUPPORTED, "unknown geometry_kind");
     if (s->n_lights < 0 || s->n_lights > kMaxLights || (s->n_lights > 0 && !s->lights))
         return fail(ctx, IPT_E_UNSUPPORTED, "n_lights out of range");

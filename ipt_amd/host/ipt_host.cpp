@@ -215,7 +215,23 @@ Scene make_scene_fractal() {
     auto camera = std::make_shared<SimpleCamera>(vec3f{0.0f, -4.0f, 0.0f}, vec3f{0, 1, 0});
     return Scene{std::make_shared<FractalSpheres>(), lighting, camera};
 }
-Scene make_scene_smallpt() { unsupported("make_scene_smallpt (GeometrySmallPt)"); }
+// GeometrySmallPt.cpp:24-33 (glm::vec3 converts each double to float)
+GeometrySmallPt::GeometrySmallPt() {
+    spheres = {{1e3, vec3f{(float)(1e3 + 1), 40.8f, 81.6f}},  {1e3, vec3f{(float)(-1e3 + 99), 40.8f, 81.6f}},
+               {1e3, vec3f{50, 40.8f, (float)1e3}},          {1e3, vec3f{50, (float)1e3, 81.6f}},
+               {1e3, vec3f{50, (float)(-1e3 + 81.6), 81.6f}}, {16.5, vec3f{27, 16.5f, 47}},
+               {16.5, vec3f{73, 16.5f, 78}}};
+}
+
+Scene make_scene_smallpt() {
+    auto lighting = std::make_shared<CollectionLighting>();
+    const vec3 lc = v3(50, (float)(81.6 - 16.5), 81.6f);
+    lighting->addSquareLight(h(lc - v3(4.0f, 0, 4.0f)), vec3f{0, -1, 0}, vec3f{8.0f, 0, 0});
+    const vec3 camera_pos = v3(50.0f, 52.0f, 295.6f);
+    const vec3 camera_dir = normalize(v3(0.0f, -0.042612f, -1.0f));
+    auto camera = std::make_shared<SimpleCamera>(h(camera_pos), h(camera_dir * 2.0f), vec3f{0, 1, 0});
+    return Scene{std::make_shared<GeometrySmallPt>(), lighting, camera};
+}
 
 Scene make_scene_by_name(const std::string& spec) {
     std::vector<std::string> f;
@@ -250,6 +266,16 @@ FlatScene flatten(const Scene& s) {
         out.scene.geometry_kind = IPT_GEOM_FLOOR;
     } else if (dynamic_cast<const GeometryCorner*>(s.geometry.get())) {
         out.scene.geometry_kind = IPT_GEOM_CORNER;
+    } else if (auto gs = dynamic_cast<const GeometrySmallPt*>(s.geometry.get())) {
+        out.scene.geometry_kind = IPT_GEOM_SMALLPT;
+        for (const auto& q : gs->spheres) {
+            ipt_sphere t{};
+            t.center[0] = q.p.x;
+            t.center[1] = q.p.y;
+            t.center[2] = q.p.z;
+            t.radius = (float)q.rad;  // 1e3 and 16.5: exact in float
+            out.spheres.push_back(t);
+        }
     } else if (auto fs = dynamic_cast<const FractalSpheres*>(s.geometry.get())) {
         out.scene.geometry_kind = IPT_GEOM_SPHERES;
         for (size_t i = 0; i < fs->rs.size(); ++i) {

@@ -16,8 +16,9 @@
 // Objects here are scene DESCRIPTIONS: nothing in this layer traces a ray on
 // the CPU. Rendering is GpuRenderer / render_samples_gpu, i.e. ipt_render on
 // a gfx950 GPU, and it throws IptError(IPT_E_DEVICE) when there is none.
-// Scene types the GPU kernels do not implement yet (§8(f) row 1: the
-// smallpt scene) throw IptError(IPT_E_UNSUPPORTED) where they are created.
+// Every sample_scenes entry and light type of the reference is supported;
+// geometry or light classes outside them throw IptError(IPT_E_UNSUPPORTED)
+// when flattened.
 #pragma once
 
 #include <cstddef>
@@ -64,6 +65,16 @@ struct GeometryFloor : Geometry {};
 struct GeometryCorner : Geometry {};
 // FractalSpheres (FractalSpheres.cpp:46-97): the generated sphere chain
 // between two r=0.5 spheres at (-2,0,0) and (2,0,0), no walls.
+// GeometrySmallPt (GeometrySmallPt.cpp:11-58): smallpt's room of 7 spheres,
+// intersected in double precision.
+struct GeometrySmallPt : Geometry {
+    struct Sphere {
+        double rad;
+        vec3f p;
+    };
+    std::vector<Sphere> spheres;
+    GeometrySmallPt();
+};
 struct FractalSpheres : Geometry {
     std::vector<float> rs;
     std::vector<vec3f> cs;
@@ -151,8 +162,7 @@ Scene make_scene_random_lights(int n, uint64_t seed = 7);  // overlapping random
 Scene make_scene_square_lit_by_square();                  // sample_scenes.cpp:73-85
 Scene make_scene_lit_corner();                            // sample_scenes.cpp:88-108
 Scene make_scene_fractal();                               // sample_scenes.cpp:43-55
-// not on the GPU path yet (§8(f) row 1): throws IptError(IPT_E_UNSUPPORTED)
-Scene make_scene_smallpt();
+Scene make_scene_smallpt();                               // sample_scenes.cpp:57-71
 // "box", "box_lights:K", "spheres:N[:SEED]", "random_lights:N[:SEED]", "fractal", ...
 Scene make_scene_by_name(const std::string& name);
 

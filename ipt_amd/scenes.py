@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .capi import (IPT_GEOM_CORNER, IPT_GEOM_FLOOR, IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES,
+from .capi import (IPT_GEOM_CORNER, IPT_GEOM_FLOOR, IPT_GEOM_SMALLPT, IPT_GEOM_SPHERE_IN_BOX, IPT_GEOM_SPHERES,
                    IPT_GEOM_SPHERES_IN_BOX, IPT_LIGHT_AREA_DIAMOND, IPT_LIGHT_AREA_TRIANGLE, IPT_LIGHT_OUTER_SPHERE,
                    IPT_LIGHT_POINT, IPT_LIGHT_SPHERE)
 
@@ -189,6 +189,32 @@ def make_scene_fractal():
     cam = simple_camera(_v(0.0, -4.0, 0.0), _v(0.0, 1.0, 0.0))
     return {"geometry_kind": IPT_GEOM_SPHERES, "lights": [sphere_light((-5.5, 0.0, 0.0), 1.0)],
             "spheres": fractal_spheres(), "camera": cam}
+
+
+def smallpt_spheres():
+    """GeometrySmallPt.cpp:24-33: smallpt's room (radius, centre), the centres
+    written as double expressions converted to float by glm::vec3."""
+    return [
+        ([1e3 + 1, 40.8, 81.6], 1e3),   # left
+        ([-1e3 + 99, 40.8, 81.6], 1e3),  # right
+        ([50, 40.8, 1e3], 1e3),          # back
+        ([50, 1e3, 81.6], 1e3),          # bottom
+        ([50, -1e3 + 81.6, 81.6], 1e3),  # top
+        ([27, 16.5, 47], 16.5),
+        ([73, 16.5, 78], 16.5),          # glass
+    ]
+
+
+def make_scene_smallpt():
+    """sample_scenes.cpp:57-71: smallpt's room lit by an 8x8 square light,
+    camera at (50,52,295.6), direction normalize((0,-0.042612,-1))*2, up +y."""
+    spheres = [([float(f32(v)) for v in c], float(f32(r))) for c, r in smallpt_spheres()]
+    lc = _v(50, 81.6 - 16.5, 81.6)
+    light = square_light((lc - _v(4.0, 0, 4.0)).astype(f32), (0.0, -1.0, 0.0), (8.0, 0.0, 0.0), 1.0)
+    camera_pos = _v(50.0, 52.0, 295.6)
+    camera_dir = normalize(_v(0.0, -0.042612, -1.0))
+    cam = simple_camera(camera_pos, (camera_dir * f32(2.0)).astype(f32), up_hint=(0.0, 1.0, 0.0))
+    return {"geometry_kind": IPT_GEOM_SMALLPT, "lights": [light], "spheres": spheres, "camera": cam}
 
 
 def make_scene_box_lights(k: int = 16):

@@ -361,6 +361,33 @@ bool geometry_trace(const SceneO& sc, V3 origin, V3 direction, SurfHit* out) {
         out->plain_cosine = true;
         return true;
     }
+    if (sc.geometry_kind == IPT_GEOM_SMALLPT) {  // GeometrySmallPt.cpp:11-58
+        double min_t = std::numeric_limits<double>::infinity();
+        int min_s = -1;
+        for (size_t i = 0; i < sc.sph_r.size(); ++i) {
+            // Sphere::intersect (GeometrySmallPt.cpp:16-22), rad a double
+            const double rad = sc.sph_r[i];
+            V3 op = sc.sph_c[i] - origin;
+            double t, eps = 1e-4, b = dot(op, direction), det = b * b - dot(op, op) + rad * rad;
+            if (det < 0) {
+                t = 0;
+            } else {
+                det = std::sqrt(det);
+                t = (t = b - det) > eps ? t : ((t = b + det) > eps ? t : 0);
+            }
+            if (t != 0.0) {
+                if (t < min_t) {
+                    min_t = t;
+                    min_s = (int)i;
+                }
+            }
+        }
+        if (!std::isfinite(min_t)) return false;
+        out->position = origin + direction * (float)min_t;
+        const V3 v = normalize(out->position - sc.sph_c[min_s]);
+        out->normal = sc.sph_r[min_s] < 100 ? v : -v;
+        return true;
+    }
     if (sc.geometry_kind == IPT_GEOM_CORNER) {  // GeometryCorner.cpp:10-42
         float tx = intersection_with_box_plane(mk(-1, 0, 0), origin, direction);
         float ty = intersection_with_box_plane(mk(0, -1, 0), origin, direction);

@@ -211,6 +211,18 @@ def test_sample_scene_fractal_bit_exact(gpu_ctx, oracle, n_rays, depth_max):
     assert (ov > 0).any()  # the sphere light reaches the camera
 
 
+@pytest.mark.parametrize("n_rays,depth_max", [(16, 8), (8, 5)])
+def test_sample_scene_smallpt_bit_exact(gpu_ctx, oracle, n_rays, depth_max):
+    """sample_scenes.cpp:57-71: smallpt's room (GeometrySmallPt, double
+    precision Sphere::intersect, flipped room normals) with a square light."""
+    desc = scenes.make_scene_smallpt()
+    p = capi.make_params(40, 32, 2, n_rays=n_rays, depth_max=depth_max)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+    assert (ov > 0).mean() > 0.05
+
+
 @pytest.mark.parametrize("geom", ["box", "fractal"])
 def test_round_lights_bit_exact(gpu_ctx, oracle, geom):
     """Sphere, point and inverted-sphere (outer) lights mixed with area lights:

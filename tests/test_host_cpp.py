@@ -55,16 +55,17 @@ def _py_flat(desc):
     ("square_lit_by_square", scenes.make_scene_square_lit_by_square),
     ("lit_corner", scenes.make_scene_lit_corner),
     ("fractal", scenes.make_scene_fractal),
+    ("smallpt", scenes.make_scene_smallpt),
 ])
 def test_cpp_scenes_match_python(dump, name, desc_fn):
     out = subprocess.run([str(dump), "scene", name], check=True, capture_output=True, text=True).stdout
     assert json.loads(out) == _py_flat(desc_fn())
 
 
-@pytest.mark.parametrize("name", ["smallpt"])
-def test_unsupported_scenes_fail_loudly(dump, name):
+@pytest.mark.parametrize("name", ["open_spheres", "nonexistent"])
+def test_unknown_scenes_fail_loudly(dump, name):
     out = subprocess.run([str(dump), "scene-error", name], check=True, capture_output=True, text=True).stdout
-    assert int(out) == capi.IPT_E_UNSUPPORTED
+    assert int(out) == capi.IPT_E_INVALID
 
 
 def _read_png_gray8(path):

@@ -198,7 +198,7 @@ def _ref_scenes():
 
 
 @pytest.mark.parametrize("idx,name", [(0, "make_scene_square_lit_by_square"), (1, "make_scene_lit_corner"),
-                                      (2, "make_scene_fractal")])
+                                      (2, "make_scene_fractal"), (3, "make_scene_smallpt")])
 def test_area_light_scenes_flattening(lib, idx, name):
     """ipt_amd.scenes reproduces sample_scenes.cpp's floor, corner and fractal
     scenes: camera fields, light fields (AreaLight, triangle AreaLight,
