@@ -231,12 +231,16 @@ int ipt_glare(ipt_ctx* ctx, const float* in, float* out, int width, int height, 
      IPT_DDF_MIXTURE UnionDdf(lights..., RotateDdf(CosineDdf, normal)) with
                      the scene's unite() weights: origin params[0..2], normal
                      params[3..5]
+     IPT_DDF_COSINE_TABLE  IPT_DDF_COSINE as the path kernel samples it, from
+                     the exact CosineDdf tables indexed by the draws' 24 bits
+                     (u1, u2 must lie on the RNG's 2^-24 grid)
    ipt_ddf_sample: u = n x {pick, u1, u2} uniforms in [0,1) -> n directions
    (vec3() where the reference's sampler returns it); ipt_ddf_value: n
    directions -> n DDF values. Host buffers. */
 #define IPT_DDF_COSINE 0
 #define IPT_DDF_LIGHT 1
 #define IPT_DDF_MIXTURE 2
+#define IPT_DDF_COSINE_TABLE 3
 int ipt_ddf_sample(ipt_ctx* ctx, int kind, const float* params, const float* u, int64_t n, float* dirs);
 int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs, int64_t n, float* values);
 

@@ -18,7 +18,7 @@ LIB_PATH = _HERE / "lib" / "libipt_hip.so"
 
 IPT_OK = 0
 IPT_E_INVALID = -1
-IPT_DDF_COSINE, IPT_DDF_LIGHT, IPT_DDF_MIXTURE = 0, 1, 2
+IPT_DDF_COSINE, IPT_DDF_LIGHT, IPT_DDF_MIXTURE, IPT_DDF_COSINE_TABLE = 0, 1, 2, 3
 IPT_E_DEVICE = -2
 IPT_E_UNSUPPORTED = -3
 IPT_E_NOSCENE = -4

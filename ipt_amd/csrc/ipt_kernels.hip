@@ -116,6 +116,8 @@ struct KParams {
     int n_light_nodes;
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
+    const float2* __restrict__ cos_a;     // [2^24] CosineDdf table by u1's 24 bits: (cos_alpha, sin(alpha))
+    const float2* __restrict__ cos_b;     // [2^24] by u2's 24 bits: (cos phi, sin phi)
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
@@ -277,9 +279,18 @@ __host__ __device__ constexpr int frame_slots(int geom) {
 // LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
 // task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
 // so unsharded launches do not allocate it).
+// CosineDdf samples from exact tables (cos_table_kernel) instead of a worker
+// pass: -DIPT_COS_TABLE=0 restores the pooled evaluation (experiments).
+#ifndef IPT_COS_TABLE
+#define IPT_COS_TABLE 1
+#endif
+#ifndef IPT_COS_NT
+#define IPT_COS_NT 0
+#endif
+constexpr int kCosTaskWords = IPT_COS_TABLE ? 0 : 3 * kBlock;
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
     return 60 + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) + 4 +
-           12 * (size_t)frame_slots(geom) + 3 * kBlock;
+           12 * (size_t)frame_slots(geom) + kCosTaskWords;
 }
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4
@@ -332,8 +343,8 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
     float* cdf_lds = weights_lds + (kLdsLights + 1);
     int* xcnt = reinterpret_cast<int*>(wallf + 60 + (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
     float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [12][kFrameSlots]
-    float* xcos = xfr + 12 * kFrameSlots;                      // [3][kBlock]
-    int* cand_lds = reinterpret_cast<int*>(xcos + 3 * kBlock);  // [kLdsCand] when kp.cand_lds
+    float* xcos = xfr + 12 * kFrameSlots;                      // [3][kBlock] (pooled cosine samples)
+    int* cand_lds = reinterpret_cast<int*>(xcos + kCosTaskWords);  // [kLdsCand] when kp.cand_lds
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     if (tid < 4) xcnt[tid] = 0;
@@ -577,7 +588,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
         const bool iter_lane = active && has_path && !have_ray && !stalled;
         int pick = -1;
-        float u1 = 0.0f, u2 = 0.0f;
+        float u1 = 0.0f, u2 = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
         if (iter_lane) {
             IPT_PHASE(3);
             if ((k >> 2) != blk) {
@@ -613,14 +624,34 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             }
             pick = c;
             if (c <= nl) {
-                u1 = u01(win_at(w, j + 1));
-                u2 = u01(win_at(w, j + 2));
+                const uint32_t r1 = win_at(w, j + 1), r2 = win_at(w, j + 2);
+                u1 = u01(r1);
+                u2 = u01(r2);
+                if (IPT_COS_TABLE && c == nl) {
+                    // CosineDdf::sample (ddf.cpp:223-231) of (u1, u2) = (cos_alpha, r) x
+                    // (cos phi, sin phi) looked up by the draws' 24 bits; consumed after
+                    // barrier B, so the loads' latency hides behind the frame pass
+#if IPT_COS_NT
+                    // streaming hint: keep the random table gathers from evicting
+                    // scene data (light BVH, sphere BVH) from L2
+                    typedef float f2v __attribute__((ext_vector_type(2)));
+                    const f2v ta = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(kp.cos_a) + (r1 >> 8));
+                    const f2v tb = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(kp.cos_b) + (r2 >> 8));
+#else
+                    const float2 ta = kp.cos_a[r1 >> 8];
+                    const float2 tb = kp.cos_b[r2 >> 8];
+#endif
+                    u1 = ta.x;
+                    u2 = ta.y;
+                    cs_c = tb.x;
+                    cs_s = tb.y;
+                }
                 k += 3;
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
             }
         }
-        const bool want_cos = iter_lane && pick == nl;
+        const bool want_cos = !IPT_COS_TABLE && iter_lane && pick == nl;
         int slot_c = 0;
         {
             const uint64_t m = __ballot(want_cos);
@@ -632,7 +663,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                 slot_c = base + __popcll(m & lanemask_lt);
             }
         }
-        if (want_cos) {
+        if (!IPT_COS_TABLE && want_cos) {
             xcos[0 * kBlock + slot_c] = u1;
             xcos[1 * kBlock + slot_c] = u2;
         }
@@ -647,7 +678,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         }
         {
             const int nf = min(xcnt[par * 2 + 0], kFrameSlots);
-            const int nc = xcnt[par * 2 + 1];
+            const int nc = IPT_COS_TABLE ? 0 : xcnt[par * 2 + 1];
             const int pf = (nf + 63) >> 6, pc = (nc + 63) >> 6;
             // passes dealt round-robin to the 4 waves, frames from wave 0 up and
             // cosine samples from wave 3 down, so a single busy wave is rare
@@ -669,7 +700,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                     }
                 } else {
                     const int sl = (pc - 1 - (pass - pf)) * 64 + lane;
-                    if (sl < nc) {
+                    if (!IPT_COS_TABLE && sl < nc) {
                         IPT_PHASE(6);
                         const vec3 v = cosine_sample_local(xcos[0 * kBlock + sl], xcos[1 * kBlock + sl]);
                         if (IPT_ABL == 2)
@@ -702,8 +733,11 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                     keep_alive(light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
                 if (COUNT) ++c_lsamp;
             } else if (pick == nl) {
-                dir = frame_apply(tfr, v3(xcos[0 * kBlock + slot_c], xcos[1 * kBlock + slot_c],
-                                          xcos[2 * kBlock + slot_c]));
+                if (IPT_COS_TABLE)  // cosine_sample_local: (r cos phi, r sin phi, cos_alpha)
+                    dir = frame_apply(tfr, v3(u2 * cs_c, u2 * cs_s, u1));
+                else
+                    dir = frame_apply(tfr, v3(xcos[0 * kBlock + slot_c], xcos[1 * kBlock + slot_c],
+                                              xcos[2 * kBlock + slot_c]));
             }
             ++ti;
             if (COUNT) ++c_iter;
@@ -1002,15 +1036,21 @@ __global__ void math_kernel(int fn, const float* in, float* out, long long n) {
 // RotateDdf(CosineDdf, normal=params[3..5]) at origin params[0..2].
 __global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ params, const LightDev* __restrict__ lights,
                            const float* __restrict__ weights, const float* __restrict__ cdf, int nl,
-                           const float* __restrict__ in, long long n, float* __restrict__ out) {
+                           const float* __restrict__ in, long long n, float* __restrict__ out,
+                           const float2* __restrict__ cos_a, const float2* __restrict__ cos_b) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const vec3 o = v3(params[0], params[1], params[2]);
+    if (kind == 3) kind = value_mode ? 0 : kind;  // table sampler: same DDF value
     if (!value_mode) {
         const float pick = in[3 * i], u1 = in[3 * i + 1], u2 = in[3 * i + 2];
         vec3 v = v3(0.0f, 0.0f, 0.0f);
         if (kind == 0) {
             v = frame_apply(make_frame(o), cosine_sample_local(u1, u2));
+        } else if (kind == 3) {
+            // the path kernel's table lookup (u on the RNG's 2^-24 grid, checked by the caller)
+            const float2 ta = cos_a[(uint32_t)(u1 * 16777216.0f)], tb = cos_b[(uint32_t)(u2 * 16777216.0f)];
+            v = frame_apply(make_frame(o), v3(ta.y * tb.x, ta.y * tb.y, ta.x));
         } else if (kind == 1) {
             v = light_sample_dir(lights[(int)params[3]], o, u1, u2);
         } else {
@@ -1043,6 +1083,23 @@ __global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ p
         }
         out[i] = v;
     }
+}
+
+// Exact CosineDdf tables (ddf.cpp:223-231) over the 2^24 values a draw can
+// take (u = i * 2^-24, ipt_math.h u01): a[i] = (sqrtf(u), sinf(acosf(sqrtf(u)))),
+// b[i] = sincosf((float)(2*M_PI*u)) as (cos, sin). cosine_sample_local(u1, u2)
+// == (a[i1].y*b[i2].x, a[i1].y*b[i2].y, a[i1].x) bit for bit (same functions,
+// same products).
+__global__ void cos_table_kernel(float2* __restrict__ a, float2* __restrict__ b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (1u << 24)) return;
+    const float u = u01(i << 8);
+    const float cos_alpha = sqrt_(u);
+    const float r = sinf_small_(acosf_(cos_alpha));
+    float sp, cp;
+    sincosf_small_(two_pi_times(u), &sp, &cp);
+    a[i] = make_float2(cos_alpha, r);
+    b[i] = make_float2(cp, sp);
 }
 
 // Exact restatement of math_fn (differs only where the device uses a fast
@@ -1110,6 +1167,8 @@ struct ipt_ctx {
     int cand_cap_rows = 0, cand_cap_h = 0;
     unsigned long long* d_unit = nullptr;
     unsigned long long* d_counters = nullptr;
+    float2* d_cos_a = nullptr;  // CosineDdf tables (cos_table_kernel), 2 x 128 MiB
+    float2* d_cos_b = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
     int blocks_per_cu = 0;
@@ -1132,6 +1191,16 @@ int fail(ipt_ctx* ctx, int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                           \
             return fail(ctx, IPT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
+
+int ensure_cos_tables(ipt_ctx* ctx, hipStream_t st) {
+    if (ctx->d_cos_a) return IPT_OK;
+    const size_t n = (size_t)1 << 24;
+    HIPCHECK(ctx, hipMalloc(&ctx->d_cos_a, n * sizeof(float2)));
+    HIPCHECK(ctx, hipMalloc(&ctx->d_cos_b, n * sizeof(float2)));
+    hipLaunchKernelGGL(cos_table_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, st, ctx->d_cos_a, ctx->d_cos_b);
+    HIPCHECK(ctx, hipGetLastError());
+    return IPT_OK;
+}
 
 int ensure_work(ipt_ctx* ctx, size_t elems, size_t npix, int H, int n_cand) {
     if (elems > ctx->work_cap) {
@@ -1230,8 +1299,21 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     HIPCHECK(ctx, hipGetLastError());
     return IPT_OK;
 }
+// -DIPT_C2_ONLY=1: experiment builds (scripts/variants.sh) instantiate the
+// sample_scenes[0] kernel alone (seconds to compile); other scenes fail loudly.
+#ifndef IPT_C2_ONLY
+#define IPT_C2_ONLY 0
+#endif
+#ifndef IPT_C2_LMODE
+#define IPT_C2_LMODE kLightsOne
+#endif
 template <int MAXSUSP, bool COUNT, int LMODE>
 int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
+    if constexpr (IPT_C2_ONLY != 0) {
+        if (MAXSUSP != 4 || LMODE != kLightsOne || kp.geometry_kind != IPT_GEOM_SPHERE_IN_BOX)
+            return fail(ctx, IPT_E_UNSUPPORTED, "IPT_C2_ONLY experiment build");
+        return launch_path4<4, COUNT, IPT_C2_LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+    } else {
     switch (kp.geometry_kind) {
         case IPT_GEOM_SPHERES_IN_BOX: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES_IN_BOX>(ctx, kp, st);
         case IPT_GEOM_FLOOR: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_FLOOR>(ctx, kp, st);
@@ -1239,6 +1321,7 @@ int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
         case IPT_GEOM_SPHERES: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERES>(ctx, kp, st);
         case IPT_GEOM_SMALLPT: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SMALLPT>(ctx, kp, st);
         default: return launch_path4<MAXSUSP, COUNT, LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+    }
     }
 }
 template <int MAXSUSP, bool COUNT>
@@ -1267,6 +1350,10 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     if (host_values) chunk = p->spp;  // debug path: one chunk
     int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
     if (rc) return rc;
+    if (IPT_COS_TABLE) {
+        rc = ensure_cos_tables(ctx, st);
+        if (rc) return rc;
+    }
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice, st));
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice, st));
     const int susp = needed_susp(p);
@@ -1312,6 +1399,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.light_nodes = ctx->d_light_nodes;
         kp.n_light_nodes = ctx->n_light_nodes;
         kp.cdf_bsearch = ctx->cdf_bsearch;
+        kp.cos_a = ctx->d_cos_a;
+        kp.cos_b = ctx->d_cos_b;
         kp.cand_lds = (p->n_shards > 1 && p->tile_rows > 0 && kp.n_cand <= kLdsCand) ? 1 : 0;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
@@ -1419,7 +1508,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
-                    ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters};
+                    ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& e : ctx->ev)
@@ -1701,7 +1790,18 @@ int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n
 static int ddf_call(ipt_ctx* ctx, int value_mode, int kind, const float* params, const float* in, int64_t n,
                     float* out) {
     if (!ctx) return IPT_E_INVALID;
-    if (!params || !in || !out || n < 0 || kind < 0 || kind > 2) return fail(ctx, IPT_E_INVALID, "ipt_ddf: bad arguments");
+    if (!params || !in || !out || n < 0 || kind < 0 || kind > 3) return fail(ctx, IPT_E_INVALID, "ipt_ddf: bad arguments");
+    if (kind == 3 && !value_mode)
+        for (int64_t i = 0; i < n; ++i)
+            for (int c = 1; c < 3; ++c) {
+                const float u = in[3 * i + c];
+                if (!(u >= 0.0f && u < 1.0f) || u * 16777216.0f != (float)(uint32_t)(u * 16777216.0f))
+                    return fail(ctx, IPT_E_INVALID, "ipt_ddf: table sampler needs u on the 2^-24 grid");
+            }
+    if (kind == 3) {
+        const int rc = ensure_cos_tables(ctx, ctx->stream);
+        if (rc) return rc;
+    }
     if (!ctx->has_scene) return fail(ctx, IPT_E_INVALID, "ipt_ddf: no scene uploaded");
     if (kind == 1 && (params[3] < 0.0f || params[3] >= (float)ctx->n_lights || params[3] != (float)(int)params[3]))
         return fail(ctx, IPT_E_INVALID, "ipt_ddf: light index out of range");
@@ -1712,12 +1812,13 @@ static int ddf_call(ipt_ctx* ctx, int value_mode, int kind, const float* params,
     HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * in_w * sizeof(float)));
     HIPCHECK(ctx, hipMalloc(&dout, std::max<int64_t>(n, 1) * out_w * sizeof(float)));
     float hp[8] = {0};
-    for (int k = 0; k < (kind == 0 ? 3 : (kind == 1 ? 4 : 6)); ++k) hp[k] = params[k];
+    for (int k = 0; k < (kind == 0 || kind == 3 ? 3 : (kind == 1 ? 4 : 6)); ++k) hp[k] = params[k];
     HIPCHECK(ctx, hipMemcpy(dp, hp, sizeof hp, hipMemcpyHostToDevice));
     HIPCHECK(ctx, hipMemcpy(din, in, n * in_w * sizeof(float), hipMemcpyHostToDevice));
     if (n > 0)
         hipLaunchKernelGGL(ddf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, value_mode, kind,
-                           dp, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->n_lights, din, (long long)n, dout);
+                           dp, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->n_lights, din, (long long)n, dout,
+                           ctx->d_cos_a, ctx->d_cos_b);
     HIPCHECK(ctx, hipGetLastError());
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHECK(ctx, hipMemcpy(out, dout, n * out_w * sizeof(float), hipMemcpyDeviceToHost));

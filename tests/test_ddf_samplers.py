@@ -118,3 +118,31 @@ def test_device_samplers_bit_exact_and_chi2(gpu_ctx, oracle, case):
     ok, info = check_ddf(d, lambda x: gpu_ctx.ddf_value(kind, params, x), N=N, strict_integral=strict,
                          **_grid(kind, params))
     assert ok, (case, info)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("to", [[0, 0, 1], [NZ, -NZ, NZ]])
+def test_cosine_table_sampler_exhaustive(gpu_ctx, oracle, to):
+    """The path kernel's CosineDdf tables (every one of the 2^24 values each of
+    u1 and u2 can take, paired by an odd-multiplier permutation) against the
+    oracle's glibc CosineDdf::sample (ddf.cpp:223-231): bit-identical. With
+    to = +z the frame is the identity, so the table entries themselves are
+    compared."""
+    gpu_ctx.upload_scene(scenes.make_scene_box())
+    n = 1 << 24 if to == [0, 0, 1] else 1 << 20
+    i1 = np.arange(n, dtype=np.uint64) * ((1 << 24) // n)
+    i2 = (i1 * 7919 + 12345) % (1 << 24)
+    u = np.zeros((n, 3), np.float32)
+    u[:, 1] = i1.astype(np.float32) * np.float32(2.0 ** -24)
+    u[:, 2] = i2.astype(np.float32) * np.float32(2.0 ** -24)
+    d = gpu_ctx.ddf_sample(capi.IPT_DDF_COSINE_TABLE, to, u)
+    o = oracle_sample(scenes.make_scene_box(), capi.IPT_DDF_COSINE, to, u)
+    bad = (_bits(d) != _bits(o)).any(1)
+    assert not bad.any(), (int(bad.sum()), u[bad][:3], d[bad][:3], o[bad][:3])
+
+
+@pytest.mark.gpu
+def test_cosine_table_sampler_rejects_off_grid(gpu_ctx):
+    gpu_ctx.upload_scene(scenes.make_scene_box())
+    with pytest.raises(capi.IptError):
+        gpu_ctx.ddf_sample(capi.IPT_DDF_COSINE_TABLE, [0, 0, 1], np.array([[0, 0.1, 0.5]], np.float32))
