@@ -43,6 +43,20 @@ namespace {
 #endif
 constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOCK for experiments)
 
+// Micro-optimisation switches (all exact; 0 restores the plain form, for A/B builds)
+#ifndef IPT_NL1
+#define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
+#endif
+#ifndef IPT_UDIV32
+#define IPT_UDIV32 1  // work-unit decomposition in 32-bit arithmetic (units < 2^32)
+#endif
+#ifndef IPT_BOXDIV
+#define IPT_BOXDIV 1  // box planes' divisions without range handling (origins within 2^39)
+#endif
+#ifndef IPT_LENCMP
+#define IPT_LENCMP 1  // length(a) > length(b) decided on the squares when they are far apart
+#endif
+
 // Profiling-only builds (-DIPT_ABL=n, scripts/ablate.sh): phase n is computed a
 // second time on a perturbed input and kept alive, so the wall-time delta is
 // that phase's marginal cost with the path tree unchanged. 0 in the product.
@@ -116,10 +130,38 @@ struct KParams {
     int n_light_nodes;
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
+    double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
+    uint32_t per_pass32;                  // n_cand*W (< 2^32)
+    int box_inrange;                      // camera and sphere list within 2^39 (box_plane_t<true>)
     const float2* __restrict__ cos_a;     // [2^24] CosineDdf table by u1's 24 bits: (cos_alpha, sin(alpha))
     const float2* __restrict__ cos_b;     // [2^24] by u2's 24 bits: (cos phi, sin phi)
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
+
+// floor(n / d) for 32-bit n, d >= 1 from a double reciprocal: the estimate's
+// error is below (n/d) * 2^-51 < 1/d (n < 2^32), i.e. below the distance of a
+// non-integer n/d from the next integer, so it truncates to the quotient or,
+// when n/d is an integer approached from below, to one less (fixed up).
+__device__ __forceinline__ uint32_t udiv_exact(uint32_t n, uint32_t d, double inv_d) {
+    uint32_t q = (uint32_t)((double)n * inv_d);
+    if (n - q * d >= d) ++q;
+    return q;
+}
+// length(a) > length(b) (glm length = sqrtf(dot), func_geometric.inl:8-14) for
+// a, b with squares x, y: sqrtf is monotone, so x <= y gives false, and
+// x > y(1+2^-20) (y normal) separates the two correctly rounded roots by more
+// than their rounding; only the rare near-ties (or NaN/tiny) take the roots.
+__device__ __forceinline__ bool longer(vec3 a, vec3 b) {
+    const float x = dot(a, a), y = dot(b, b);
+    if (!IPT_LENCMP) return sqrt_(x) > sqrt_(y);
+    const bool far_gt = x > y * 1.000001907f && y >= 1e-30f;  // 1 + 2^-19
+    const bool le = x <= y;
+    const bool tie = !far_gt && !le;
+    bool r = far_gt;
+    if (__builtin_expect(__any(tie), 0))
+        if (tie) r = sqrt_(x) > sqrt_(y);
+    return r;
+}
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
     if (kp.n_shards <= 1 || kp.tile_rows <= 0) return true;
@@ -169,7 +211,10 @@ __device__ __forceinline__ float safe_rcp(float d) {
 template <bool COUNT, int GEOM>
 __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 d, int* prim, uint32_t& c_nodes,
                                                 uint32_t& c_tests) {
-    if (GEOM == IPT_GEOM_SPHERE_IN_BOX) return trace_box(o, d, prim);
+    // kp.box_inrange: every ray origin (camera, wall/floor hits, listed spheres)
+    // lies within 2^39, so the planes' divisions take the range-free sequence
+    if (GEOM == IPT_GEOM_SPHERE_IN_BOX)
+        return (IPT_BOXDIV && kp.box_inrange) ? trace_box<true>(o, d, prim) : trace_box<false>(o, d, prim);
     if (GEOM == IPT_GEOM_FLOOR) {  // GeometryFloor.cpp:11-13
         const float t = box_plane_t(o.z, d.z, -1.0f, o, d);
         *prim = t == inf_() ? -1 : 0;
@@ -217,7 +262,8 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
     // lowest index among equal t, and a sphere never wins a tie with a plane.
     int p = -1;
     float best = inf_();  // FractalSpheres: no walls
-    if (GEOM == IPT_GEOM_SPHERES_IN_BOX) best = trace_box_planes_only(o, d, &p);
+    if (GEOM == IPT_GEOM_SPHERES_IN_BOX)
+        best = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(o, d, &p) : trace_box_planes_only<false>(o, d, &p);
     int bidx = -1;
     if (kp.n_nodes > 0) {
         const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
@@ -379,7 +425,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
 
     const int lane = tid & 63;
     const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int nl = kp.n_lights;
+    const int nl = (IPT_NL1 && LMODE == kLightsOne) ? 1 : kp.n_lights;
     const float w_sdf = kp.weights[nl];
     const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
     // n at every depth is n_rays >> d; when n_rays is a power of two, res/n ==
@@ -500,10 +546,18 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         if (active && has_path && fresh) {
             IPT_PHASE(2);
             fresh = false;
+#if IPT_UDIV32
+            const uint32_t u32 = (uint32_t)unit;
+            const uint32_t s = udiv_exact(u32, kp.per_pass32, kp.inv_per_pass);
+            const uint32_t rem = u32 - s * kp.per_pass32;
+            const int cand = (int)udiv_exact(rem, (uint32_t)kp.W, kp.inv_w);
+            const int ix = (int)(rem - (uint32_t)cand * (uint32_t)kp.W);
+#else
             const unsigned long long s = unit / per_pass;
             const unsigned long long rem = unit - s * per_pass;
             const int cand = (int)(rem / (unsigned long long)kp.W);
             const int ix = (int)(rem - (unsigned long long)cand * kp.W);
+#endif
             int iy = cand;
             if (sharded) {
                 if (cand_in_lds)
@@ -773,7 +827,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                 }
                 if (COUNT) ++c_ltest;
                 if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp, hn);
-                if (h && (!has_li || length(li_pos - ro) > length(hp - ro))) {
+                if (h && (!has_li || longer(li_pos - ro, hp - ro))) {
                     has_li = true;
                     li_pos = hp;
                     li_pow = L.spow;
@@ -830,7 +884,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                     c_light += has_li ? 1u : 0u;
                 }
                 if (has_si) si_pos = ro + rd * t;
-                if (has_li && (!has_si || length(si_pos - ro) > length(li_pos - ro))) {
+                if (has_li && (!has_si || longer(si_pos - ro, li_pos - ro))) {
                     cv = isfinite_(li_pow) ? li_pow : 1.0f;
                 } else if (!has_si) {
                     cv = 0.0f;
@@ -1156,6 +1210,7 @@ struct ipt_ctx {
     bool any_round_light = false;
     int bpc_override = 0;
     vec3 cam_pos, cam_dir, cam_right, cam_up;
+    int box_inrange = 0;
     // work buffers
     float* d_values = nullptr;
     uint8_t* d_codes = nullptr;
@@ -1376,6 +1431,11 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.n_shards = p->n_shards;
         kp.shard_id = p->shard_id;
         kp.total_units = (unsigned long long)ns * per_pass;
+        if (kp.total_units >= (1ull << 32)) return fail(ctx, IPT_E_INVALID, "more than 2^32 work units in one launch");
+        kp.per_pass32 = (uint32_t)per_pass;
+        kp.box_inrange = ctx->box_inrange;
+        kp.inv_per_pass = 1.0 / (double)per_pass;
+        kp.inv_w = 1.0 / (double)W;
         kp.unit_counter = ctx->d_unit;
         kp.values = ctx->d_values;
         kp.codes = ctx->d_codes;
@@ -1646,6 +1706,10 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->cam_dir = v3(c.direction[0], c.direction[1], c.direction[2]);
     ctx->cam_right = v3(c.right[0], c.right[1], c.right[2]);
     ctx->cam_up = v3(c.up[0], c.up[1], c.up[2]);
+    // every ray origin (camera, surface points within B) inside 2^39: the box
+    // planes may use the range-free division (box_plane_t<true>)
+    const float lim = 549755813888.0f;  // 2^39
+    ctx->box_inrange = B < lim && std::fabs(cam[0]) < lim && std::fabs(cam[1]) < lim && std::fabs(cam[2]) < lim;
     ctx->has_scene = true;
     return IPT_OK;
 }

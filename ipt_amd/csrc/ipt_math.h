@@ -100,6 +100,24 @@ IPT_HD float div_(float a, float b) {
     return a / b;
 }
 
+// a/b without the range handling of the compiler's sequence (no v_div_scale /
+// v_div_fmas / v_div_fixup): the reciprocal, one Newton step and two quotient
+// residual steps. Bit-identical to a/b when |a| in [2^-40, 2^41) or a = +-0
+// (then a signed zero, whose sign the callers never observe) and |b| in
+// [2^-40, 2^41): the device proof is ipt_math_selfcheck fn 9 (2^32 pairs).
+// Callers must guarantee the range.
+IPT_HD float div_inrange_(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float y = __builtin_amdgcn_rcpf(b);
+    y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+    const float q0 = a * y;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+    return __builtin_fmaf(__builtin_fmaf(-b, q1, a), y, q1);
+#else
+    return a / b;
+#endif
+}
+
 // ------------------------------------------------------------------ vec3
 // glm::vec3 with glm's component-wise operators; no FMA anywhere.
 struct vec3 {

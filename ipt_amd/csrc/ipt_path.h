@@ -98,10 +98,15 @@ IPT_HD vec3 cosine_sample_local(float u1, float u2) {
 // dot(d, sgn*e_a) == sgn*d_a and dot(o, sgn*e_a) == sgn*o_a exactly whenever
 // the result is used (the discarded zero products only change the sign of a
 // zero, and a zero dot is rejected by the |.|<1e-6 test); d is finite.
+// INRANGE: the caller guarantees |o| < 2^39 componentwise; then the numerator
+// 1 - sgn*oa is 0 or in [2^-24, 2^40) (1 - oa is exact near 1) and the divisor
+// in [1e-6, 2): the range-free division is exact (div_inrange_); a zero
+// numerator gives t = +-0, rejected below either way.
+template <bool INRANGE = false>
 IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
     const float dp = sgn * da;
     if (lt_1em6(fabs_(dp))) return inf_();
-    const float t = div_(1.0f - sgn * oa, dp);
+    const float t = INRANGE ? div_inrange_(1.0f - sgn * oa, dp) : div_(1.0f - sgn * oa, dp);
     const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
     if (fabs_(px) > 1.0f || fabs_(py) > 1.0f || fabs_(pz) > 1.0f) return inf_();
     if (dp < 0.0f) return inf_();
@@ -133,6 +138,7 @@ IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
 // GeometrySphereInBox::traceRay (GeometrySphereInBox.cpp:10-81) nearest hit:
 // returns t (inf = miss) and the hit primitive: 0..4 = plane index in the
 // reference's order {+x,+y,+z,-x,-z}, 5 = the r=0.5 sphere.
+template <bool INRANGE = false>
 IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
     float best = inf_();
     int bi = -1;
@@ -143,18 +149,18 @@ IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
     // x: the facing plane is +x (index 0) for d.x>0 and -x (index 3) otherwise
     {
         const float s = d.x > 0.0f ? 1.0f : -1.0f;
-        const float t = box_plane_t(o.x, d.x, s, o, d);
+        const float t = box_plane_t<INRANGE>(o.x, d.x, s, o, d);
         const int i = d.x > 0.0f ? 0 : 3;
         best = t;
         bi = i;
     }
     {
-        const float t = d.y > 0.0f ? box_plane_t(o.y, d.y, 1.0f, o, d) : inf_();
+        const float t = d.y > 0.0f ? box_plane_t<INRANGE>(o.y, d.y, 1.0f, o, d) : inf_();
         if (t < best || (t == best && 1 < bi && t != inf_())) { best = t; bi = 1; }
     }
     {
         const float s = d.z > 0.0f ? 1.0f : -1.0f;
-        const float t = box_plane_t(o.z, d.z, s, o, d);
+        const float t = box_plane_t<INRANGE>(o.z, d.z, s, o, d);
         const int i = d.z > 0.0f ? 2 : 4;
         if (t < best || (t == best && i < bi && t != inf_())) { best = t; bi = i; }
     }
@@ -162,9 +168,10 @@ IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
     *prim = bi;
     return best;
 }
+template <bool INRANGE = false>
 IPT_HD float trace_box(vec3 o, vec3 d, int* prim) {
     int bi;
-    float best = trace_box_planes_only(o, d, &bi);
+    float best = trace_box_planes_only<INRANGE>(o, d, &bi);
     const float ts = sphere_t(0.5f, o, d);
     if (ts < best) { best = ts; bi = 5; }
     *prim = bi;
