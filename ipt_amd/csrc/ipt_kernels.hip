@@ -539,79 +539,12 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         }
 
         IPT_STAMP_AT(2);  // finalize + pop
-        // ------------------------- phase 2: new path (render_sample body, main.cpp:192-211)
-        bool have_ray = false, is_iter = false;
-        vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
-        int rdepth = 0;
-        if (active && has_path && fresh) {
-            IPT_PHASE(2);
-            fresh = false;
-#if IPT_UDIV32
-            const uint32_t u32 = (uint32_t)unit;
-            const uint32_t s = udiv_exact(u32, kp.per_pass32, kp.inv_per_pass);
-            const uint32_t rem = u32 - s * kp.per_pass32;
-            const int cand = (int)udiv_exact(rem, (uint32_t)kp.W, kp.inv_w);
-            const int ix = (int)(rem - (uint32_t)cand * (uint32_t)kp.W);
-#else
-            const unsigned long long s = unit / per_pass;
-            const unsigned long long rem = unit - s * per_pass;
-            const int cand = (int)(rem / (unsigned long long)kp.W);
-            const int ix = (int)(rem - (unsigned long long)cand * kp.W);
-#endif
-            int iy = cand;
-            if (sharded) {
-                if (cand_in_lds)
-                    iy = cand_lds[cand];
-                else
-                    iy = kp.cand_rows[cand];
-            }
-            rpass = (uint32_t)(kp.spp_offset + (int)s);
-            rpix = (uint32_t)(iy * kp.W + ix);
-            philox_fill(w.a0, w.a1, w.a2, w.a3, 0u, rpass, rpix, kp.key0, kp.key1);
-            blk = 0;
-            need_b = true;  // block 1 is produced by the window refill of the next iteration
-            k = 2;
-            const float x = jitter_coord(ix, u01(w.a0), kp.W);
-            const float y = jitter_coord(iy, u01(w.a1), kp.H);
-            int xi, yi;
-            grid_index(x, y, kp.W, kp.H, &xi, &yi);
-            const int yn = nominal_row(iy, kp.H);
-            const int dx = xi - ix, dy = yi - yn;
-            uint8_t code = 0xff;
-            if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < kp.W && yi < kp.H)
-                code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
-            if (code != 0x05 && code != 0xff) {
-                kp.flags[(size_t)yn * kp.W + ix] = 1;
-                kp.flags[(size_t)yi * kp.W + xi] = 1;
-                if (COUNT) ++c_drift;
-            }
-            if (code == 0xff || !owned_row(kp, yi)) {
-                // not ours (halo row of another shard) or out of range
-                kp.values[unit] = 0.0f;
-                kp.codes[unit] = code == 0xff ? code : (uint8_t)0xfe;
-                has_path = false;
-            } else {
-                kp.codes[unit] = code;
-                ro = kp.cam_pos;
-                rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
-                if (IPT_ABL == 6) {
-                    uint32_t q0, q1, q2, q3;
-                    philox_fill(q0, q1, q2, q3, (uint32_t)kp.abl_zero, rpass, rpix, kp.key0, kp.key1);
-                    keep_alive(q0 ^ q1);
-                    keep_alive(camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x + kp.abl_zero, y));
-                }
-                rdepth = 0;
-                have_ray = true;
-                if (COUNT) ++c_paths;
-            }
-        }
-
-        IPT_STAMP_AT(3);  // new path
+        IPT_STAMP_AT(3);  // (new path: after barrier B)
         // ------------- phase 3: post the step's expensive, divergent tasks to the
         // workgroup (RotateDdf frames of sphere nodes, CosineDdf local samples) so
         // that they run on ceil(N/64) dense wave-passes instead of on every wave.
         const int par = step & 1;
-        bool want_frame = need_frame && has_path;
+        bool want_frame = need_frame && has_path && !fresh;
         int slot_f = 0;
         {
             const uint64_t m = __ballot(want_frame);
@@ -640,7 +573,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             xfr[2 * kFrameSlots + slot_f] = nrm.z;
         }
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
-        const bool iter_lane = active && has_path && !have_ray && !stalled;
+        const bool iter_lane = active && has_path && !fresh && !stalled;
         int pick = -1;
         float u1 = 0.0f, u2 = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
         if (iter_lane) {
@@ -775,6 +708,74 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             tfr.m2 = v3(xfr[6 * kFrameSlots + slot_f], xfr[7 * kFrameSlots + slot_f], xfr[8 * kFrameSlots + slot_f]);
             tfr.iz = v3(xfr[9 * kFrameSlots + slot_f], xfr[10 * kFrameSlots + slot_f], xfr[11 * kFrameSlots + slot_f]);
             need_frame = false;
+        }
+
+        bool have_ray = false, is_iter = false;
+        vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
+        int rdepth = 0;
+        // ------------- phase 2: new path (render_sample body, main.cpp:192-211), after
+        // barrier B so that its camera ray is not live across the worker pass
+        if (active && has_path && fresh) {
+            IPT_PHASE(2);
+            fresh = false;
+#if IPT_UDIV32
+            const uint32_t u32 = (uint32_t)unit;
+            const uint32_t s = udiv_exact(u32, kp.per_pass32, kp.inv_per_pass);
+            const uint32_t rem = u32 - s * kp.per_pass32;
+            const int cand = (int)udiv_exact(rem, (uint32_t)kp.W, kp.inv_w);
+            const int ix = (int)(rem - (uint32_t)cand * (uint32_t)kp.W);
+#else
+            const unsigned long long s = unit / per_pass;
+            const unsigned long long rem = unit - s * per_pass;
+            const int cand = (int)(rem / (unsigned long long)kp.W);
+            const int ix = (int)(rem - (unsigned long long)cand * kp.W);
+#endif
+            int iy = cand;
+            if (sharded) {
+                if (cand_in_lds)
+                    iy = cand_lds[cand];
+                else
+                    iy = kp.cand_rows[cand];
+            }
+            rpass = (uint32_t)(kp.spp_offset + (int)s);
+            rpix = (uint32_t)(iy * kp.W + ix);
+            philox_fill(w.a0, w.a1, w.a2, w.a3, 0u, rpass, rpix, kp.key0, kp.key1);
+            blk = 0;
+            need_b = true;  // block 1 is produced by the window refill of the next iteration
+            k = 2;
+            const float x = jitter_coord(ix, u01(w.a0), kp.W);
+            const float y = jitter_coord(iy, u01(w.a1), kp.H);
+            int xi, yi;
+            grid_index(x, y, kp.W, kp.H, &xi, &yi);
+            const int yn = nominal_row(iy, kp.H);
+            const int dx = xi - ix, dy = yi - yn;
+            uint8_t code = 0xff;
+            if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < kp.W && yi < kp.H)
+                code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
+            if (code != 0x05 && code != 0xff) {
+                kp.flags[(size_t)yn * kp.W + ix] = 1;
+                kp.flags[(size_t)yi * kp.W + xi] = 1;
+                if (COUNT) ++c_drift;
+            }
+            if (code == 0xff || !owned_row(kp, yi)) {
+                // not ours (halo row of another shard) or out of range
+                kp.values[unit] = 0.0f;
+                kp.codes[unit] = code == 0xff ? code : (uint8_t)0xfe;
+                has_path = false;
+            } else {
+                kp.codes[unit] = code;
+                ro = kp.cam_pos;
+                rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
+                if (IPT_ABL == 6) {
+                    uint32_t q0, q1, q2, q3;
+                    philox_fill(q0, q1, q2, q3, (uint32_t)kp.abl_zero, rpass, rpix, kp.key0, kp.key1);
+                    keep_alive(q0 ^ q1);
+                    keep_alive(camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x + kp.abl_zero, y));
+                }
+                rdepth = 0;
+                have_ray = true;
+                if (COUNT) ++c_paths;
+            }
         }
 
         // ------------------------- phase 3b: the iteration's direction (main.cpp:149-163)
