@@ -325,18 +325,13 @@ __host__ __device__ constexpr int frame_slots(int geom) {
 // LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
 // task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
 // so unsharded launches do not allocate it).
-// CosineDdf samples from exact tables (cos_table_kernel) instead of a worker
-// pass: -DIPT_COS_TABLE=0 restores the pooled evaluation (experiments).
-#ifndef IPT_COS_TABLE
-#define IPT_COS_TABLE 1
-#endif
-#ifndef IPT_COS_NT
-#define IPT_COS_NT 0
-#endif
-constexpr int kCosTaskWords = IPT_COS_TABLE ? 0 : 3 * kBlock;
+// CosineDdf samples come from exact tables (cos_table_kernel).
+// Frames live in LDS, [12][kFrameStride]: column tid is the lane's current
+// sphere-node frame, columns kBlock..kBlock+4 the five wall frames.
+constexpr int kFrameStride = kBlock + 8;
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
-    return 60 + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) + 4 +
-           12 * (size_t)frame_slots(geom) + kCosTaskWords;
+    return 12 * (size_t)kFrameStride + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) +
+           4 + 4 * (size_t)frame_slots(geom);
 }
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4
@@ -383,20 +378,20 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
     constexpr int kFrameSlots = frame_slots(GEOM);
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
-    float* wallf = lds + MAXSUSP * kStackFields * kBlock;     // [5][12]
-    LightDev* lights_lds = reinterpret_cast<LightDev*>(wallf + 60);
-    float* weights_lds = wallf + 60 + kLdsLights * kLightWords;
+    float* lfr = lds + MAXSUSP * kStackFields * kBlock;       // [12][kFrameStride] lane + wall frames
+    LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride);
+    float* weights_lds = reinterpret_cast<float*>(lights_lds) + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
-    int* xcnt = reinterpret_cast<int*>(wallf + 60 + (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
-    float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [12][kFrameSlots]
-    float* xcos = xfr + 12 * kFrameSlots;                      // [3][kBlock] (pooled cosine samples)
-    int* cand_lds = reinterpret_cast<int*>(xcos + kCosTaskWords);  // [kLdsCand] when kp.cand_lds
+    int* xcnt = reinterpret_cast<int*>(reinterpret_cast<float*>(lights_lds) +
+                                       (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
+    float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [4][kFrameSlots] frame tasks: normal, lane
+    int* cand_lds = reinterpret_cast<int*>(xfr + 4 * kFrameSlots);  // [kLdsCand] when kp.cand_lds
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     if (tid < 4) xcnt[tid] = 0;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
     const bool cand_in_lds = kp.cand_lds != 0;
-    if (tid < 60) wallf[tid] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
+    if (tid < 60) lfr[(tid % 12) * kFrameStride + kBlock + tid / 12] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
     if (LMODE == kLightsLds) {
         const float* src = reinterpret_cast<const float*>(kp.lights);
         float* dst = reinterpret_cast<float*>(lights_lds);
@@ -446,7 +441,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
     vec3 tpos = v3(0, 0, 0);
-    Frame tfr;
+    int fdepth = -1;  // depth of the sphere node whose frame is in the lane's column
     float tres = 0.0f;
     int ti = 0, tdepth = 0, tkind = 0;  // kind: 0..4 wall plane, 5 box sphere, 6+i extra sphere i
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
@@ -525,16 +520,9 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                 ti = meta & 0xff;
                 tkind = meta >> 8;
                 tdepth = lvl;
-                if (tkind < 5) {
-                    const float* f = wallf + tkind * 12;
-                    tfr.m0 = v3(f[0], f[1], f[2]);
-                    tfr.m1 = v3(f[3], f[4], f[5]);
-                    tfr.m2 = v3(f[6], f[7], f[8]);
-                    tfr.iz = v3(f[9], f[10], f[11]);
-                    need_frame = false;
-                } else {
-                    need_frame = true;
-                }
+                // a sphere node's frame is still in the lane's column unless a
+                // sphere descendant has overwritten it
+                need_frame = tkind >= 5 && fdepth != lvl;
             }
         }
 
@@ -571,6 +559,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             xfr[0 * kFrameSlots + slot_f] = nrm.x;
             xfr[1 * kFrameSlots + slot_f] = nrm.y;
             xfr[2 * kFrameSlots + slot_f] = nrm.z;
+            xfr[3 * kFrameSlots + slot_f] = __int_as_float(tid);
         }
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
         const bool iter_lane = active && has_path && !fresh && !stalled;
@@ -614,20 +603,13 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                 const uint32_t r1 = win_at(w, j + 1), r2 = win_at(w, j + 2);
                 u1 = u01(r1);
                 u2 = u01(r2);
-                if (IPT_COS_TABLE && c == nl) {
+                if (c == nl) {
                     // CosineDdf::sample (ddf.cpp:223-231) of (u1, u2) = (cos_alpha, r) x
                     // (cos phi, sin phi) looked up by the draws' 24 bits; consumed after
                     // barrier B, so the loads' latency hides behind the frame pass
-#if IPT_COS_NT
-                    // streaming hint: keep the random table gathers from evicting
-                    // scene data (light BVH, sphere BVH) from L2
-                    typedef float f2v __attribute__((ext_vector_type(2)));
-                    const f2v ta = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(kp.cos_a) + (r1 >> 8));
-                    const f2v tb = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(kp.cos_b) + (r2 >> 8));
-#else
+                    // (a non-temporal hint measured slower on C2 and C5)
                     const float2 ta = kp.cos_a[r1 >> 8];
                     const float2 tb = kp.cos_b[r2 >> 8];
-#endif
                     u1 = ta.x;
                     u2 = ta.y;
                     cs_c = tb.x;
@@ -637,22 +619,6 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
             }
-        }
-        const bool want_cos = !IPT_COS_TABLE && iter_lane && pick == nl;
-        int slot_c = 0;
-        {
-            const uint64_t m = __ballot(want_cos);
-            if (m) {
-                const int first = __ffsll((long long)m) - 1;
-                int base = 0;
-                if (lane == first) base = atomicAdd(&xcnt[par * 2 + 1], __popcll(m));
-                base = __shfl(base, first);
-                slot_c = base + __popcll(m & lanemask_lt);
-            }
-        }
-        if (!IPT_COS_TABLE && want_cos) {
-            xcos[0 * kBlock + slot_c] = u1;
-            xcos[1 * kBlock + slot_c] = u2;
         }
         if (IPT_PROF && wave == 0) { IPT_PHASE(11); }  // workgroup steps (one wave counts)
         IPT_STAMP_AT(4);  // task posting, iteration prologue, Philox
@@ -664,38 +630,22 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             xcnt[(1 - par) * 2 + 1] = 0;
         }
         {
+            // frame passes dealt round-robin to the 4 waves; results go straight
+            // into the requesting lane's frame column
             const int nf = min(xcnt[par * 2 + 0], kFrameSlots);
-            const int nc = IPT_COS_TABLE ? 0 : xcnt[par * 2 + 1];
-            const int pf = (nf + 63) >> 6, pc = (nc + 63) >> 6;
-            // passes dealt round-robin to the 4 waves, frames from wave 0 up and
-            // cosine samples from wave 3 down, so a single busy wave is rare
-            for (int pass = wave; pass < pf + pc; pass += kBlock / 64) {
-                if (pass < pf) {
-                    const int sl = pass * 64 + lane;
-                    if (sl < nf) {
-                        IPT_PHASE(5);
-                        const vec3 nn = normalize(v3(xfr[0 * kFrameSlots + sl], xfr[1 * kFrameSlots + sl],
-                                                     xfr[2 * kFrameSlots + sl]));
-                        const Frame f = make_frame(nn);
-                        if (IPT_ABL == 1) keep_alive(make_frame(nn * (1.0f + kp.abl_zero)));
-                        xfr[0 * kFrameSlots + sl] = f.m0.x; xfr[1 * kFrameSlots + sl] = f.m0.y;
-                        xfr[2 * kFrameSlots + sl] = f.m0.z; xfr[3 * kFrameSlots + sl] = f.m1.x;
-                        xfr[4 * kFrameSlots + sl] = f.m1.y; xfr[5 * kFrameSlots + sl] = f.m1.z;
-                        xfr[6 * kFrameSlots + sl] = f.m2.x; xfr[7 * kFrameSlots + sl] = f.m2.y;
-                        xfr[8 * kFrameSlots + sl] = f.m2.z; xfr[9 * kFrameSlots + sl] = f.iz.x;
-                        xfr[10 * kFrameSlots + sl] = f.iz.y; xfr[11 * kFrameSlots + sl] = f.iz.z;
-                    }
-                } else {
-                    const int sl = (pc - 1 - (pass - pf)) * 64 + lane;
-                    if (!IPT_COS_TABLE && sl < nc) {
-                        IPT_PHASE(6);
-                        const vec3 v = cosine_sample_local(xcos[0 * kBlock + sl], xcos[1 * kBlock + sl]);
-                        if (IPT_ABL == 2)
-                            keep_alive(cosine_sample_local(xcos[0 * kBlock + sl] + kp.abl_zero, xcos[1 * kBlock + sl]));
-                        xcos[0 * kBlock + sl] = v.x;
-                        xcos[1 * kBlock + sl] = v.y;
-                        xcos[2 * kBlock + sl] = v.z;
-                    }
+            for (int sl = wave * 64 + lane; sl < ((nf + 63) & ~63); sl += kBlock) {
+                if (sl < nf) {
+                    IPT_PHASE(5);
+                    const vec3 nn = normalize(v3(xfr[0 * kFrameSlots + sl], xfr[1 * kFrameSlots + sl],
+                                                 xfr[2 * kFrameSlots + sl]));
+                    const int col = __float_as_int(xfr[3 * kFrameSlots + sl]);
+                    const Frame f = make_frame(nn);
+                    if (IPT_ABL == 1) keep_alive(make_frame(nn * (1.0f + kp.abl_zero)));
+                    float* c = lfr + col;
+                    c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
+                    c[3 * kFrameStride] = f.m1.x; c[4 * kFrameStride] = f.m1.y; c[5 * kFrameStride] = f.m1.z;
+                    c[6 * kFrameStride] = f.m2.x; c[7 * kFrameStride] = f.m2.y; c[8 * kFrameStride] = f.m2.z;
+                    c[9 * kFrameStride] = f.iz.x; c[10 * kFrameStride] = f.iz.y; c[11 * kFrameStride] = f.iz.z;
                 }
             }
         }
@@ -703,12 +653,11 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         __syncthreads();  // barrier B: results visible
         IPT_STAMP_AT(7);  // barrier B
         if (want_frame && !stalled) {
-            tfr.m0 = v3(xfr[0 * kFrameSlots + slot_f], xfr[1 * kFrameSlots + slot_f], xfr[2 * kFrameSlots + slot_f]);
-            tfr.m1 = v3(xfr[3 * kFrameSlots + slot_f], xfr[4 * kFrameSlots + slot_f], xfr[5 * kFrameSlots + slot_f]);
-            tfr.m2 = v3(xfr[6 * kFrameSlots + slot_f], xfr[7 * kFrameSlots + slot_f], xfr[8 * kFrameSlots + slot_f]);
-            tfr.iz = v3(xfr[9 * kFrameSlots + slot_f], xfr[10 * kFrameSlots + slot_f], xfr[11 * kFrameSlots + slot_f]);
             need_frame = false;
+            fdepth = tdepth;
         }
+        // the current node's frame: its wall column or the lane's own column
+        const float* frc = lfr + (tkind < 5 ? kBlock + tkind : tid);
 
         bool have_ray = false, is_iter = false;
         vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
@@ -788,11 +737,12 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                     keep_alive(light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
                 if (COUNT) ++c_lsamp;
             } else if (pick == nl) {
-                if (IPT_COS_TABLE)  // cosine_sample_local: (r cos phi, r sin phi, cos_alpha)
-                    dir = frame_apply(tfr, v3(u2 * cs_c, u2 * cs_s, u1));
-                else
-                    dir = frame_apply(tfr, v3(xcos[0 * kBlock + slot_c], xcos[1 * kBlock + slot_c],
-                                              xcos[2 * kBlock + slot_c]));
+                Frame fm;
+                fm.m0 = v3(frc[0 * kFrameStride], frc[1 * kFrameStride], frc[2 * kFrameStride]);
+                fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
+                fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
+                // cosine_sample_local from the tables: (r cos phi, r sin phi, cos_alpha)
+                dir = frame_apply(fm, v3(u2 * cs_c, u2 * cs_s, u1));
             }
             ++ti;
             if (COUNT) ++c_iter;
@@ -860,7 +810,9 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             IPT_STAMP_AT(9);  // light traces + pdf
             float mult = 0.0f;
             if (is_iter) {
-                const float sdf_val = frame_cosine_value(tfr, rd);
+                Frame fz;
+                fz.iz = v3(frc[9 * kFrameStride], frc[10 * kFrameStride], frc[11 * kFrameStride]);
+                const float sdf_val = frame_cosine_value(fz, rd);
                 const float mix = lmix + w_sdf * sdf_val;
                 mult = div_(sdf_val, mix);
             }
@@ -913,14 +865,8 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                 }
                 tpos = si_pos;
                 tkind = prim;
-                if (prim < 5) {
-                    const float* f = wallf + prim * 12;
-                    tfr.m0 = v3(f[0], f[1], f[2]);
-                    tfr.m1 = v3(f[3], f[4], f[5]);
-                    tfr.m2 = v3(f[6], f[7], f[8]);
-                    tfr.iz = v3(f[9], f[10], f[11]);
-                } else {
-                    need_frame = true;  // built in phase 2 of the next step
+                if (prim >= 5) {
+                    need_frame = true;  // built by the frame pass of the next step
                     if (COUNT) ++c_sframe;
                 }
                 tres = 0.0f;
@@ -1406,10 +1352,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     if (host_values) chunk = p->spp;  // debug path: one chunk
     int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
     if (rc) return rc;
-    if (IPT_COS_TABLE) {
-        rc = ensure_cos_tables(ctx, st);
-        if (rc) return rc;
-    }
+    rc = ensure_cos_tables(ctx, st);
+    if (rc) return rc;
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice, st));
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice, st));
     const int susp = needed_susp(p);
