@@ -53,6 +53,12 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_BOXDIV
 #define IPT_BOXDIV 1  // box planes' divisions without range handling (origins within 2^39)
 #endif
+#ifndef IPT_RESUME
+#define IPT_RESUME 1  // sphere-BVH walks bounded per step and resumed in later steps
+#endif
+#ifndef IPT_WALK_BUDGET
+#define IPT_WALK_BUDGET 48  // node visits per lane per step of a resumable walk
+#endif
 #ifndef IPT_LENCMP
 #define IPT_LENCMP 1  // length(a) > length(b) decided on the squares when they are far apart
 #endif
@@ -206,6 +212,42 @@ __device__ __forceinline__ float safe_rcp(float d) {
     return d == 0.0f ? (f2u(d) >> 31 ? -1e30f : 1e30f) : __builtin_amdgcn_rcpf(d);
 }
 
+// Stackless walk of the sphere BVH (ipt_bvh.h) from node i for at most
+// `budget` node visits; i == kp.n_nodes when the walk is complete. best/bidx
+// carry the nearest accepted hit (FractalSpheres.cpp:75-84's rule: minimal t,
+// lowest original index on ties, never replacing an equal plane hit).
+template <bool COUNT>
+__device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 d, int& i, float& best, int& bidx,
+                                                int budget, uint32_t& c_nodes, uint32_t& c_tests) {
+    const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    // near-child-first linearisation for this direction octant (ipt_bvh.h)
+    const int oct = (int)(f2u(d.x) >> 31) | (int)(f2u(d.y) >> 31) << 1 | (int)(f2u(d.z) >> 31) << 2;
+    const BvhNode* __restrict__ nodes = kp.bvh_nodes + (size_t)oct * kp.n_nodes;
+    while (i < kp.n_nodes && budget-- > 0) {
+        const BvhNode nd = nodes[i];
+        if (COUNT) ++c_nodes;
+        const float te = bvh_box_entry(nd, o, inv);
+        // te == inf is a miss; it must not pass when best is inf too (open floor)
+        const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f;
+        if (enter && nd.leaf >= 0) {
+            const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
+            if (COUNT) c_tests += (uint32_t)cnt;
+            for (int k2 = 0; k2 < cnt; ++k2) {
+                const BvhSphere sp = kp.bvh_prims[first + k2];
+                const float t = sphere_t(sp.r, o - v3(sp.c[0], sp.c[1], sp.c[2]), d);
+                if (isfinite_(t) && gt_1em6(fabs_(t)) &&
+                    (t < best || (t == best && bidx >= 0 && sp.index < bidx))) {
+                    best = t;
+                    bidx = sp.index;
+                }
+            }
+            i = nd.skip;
+        } else {
+            i = enter ? i + 1 : nd.skip;
+        }
+    }
+}
+
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
 // r=0.5 sphere, 6+i extra sphere i (original index), -1 miss.
 template <bool COUNT, int GEOM>
@@ -266,34 +308,8 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
         best = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(o, d, &p) : trace_box_planes_only<false>(o, d, &p);
     int bidx = -1;
     if (kp.n_nodes > 0) {
-        const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
-        // near-child-first linearisation for this direction octant (ipt_bvh.h)
-        const int oct = (int)(f2u(d.x) >> 31) | (int)(f2u(d.y) >> 31) << 1 | (int)(f2u(d.z) >> 31) << 2;
-        const BvhNode* __restrict__ nodes = kp.bvh_nodes + (size_t)oct * kp.n_nodes;
         int i = 0;
-        while (i < kp.n_nodes) {
-            const BvhNode nd = nodes[i];
-            if (COUNT) ++c_nodes;
-            const float te = bvh_box_entry(nd, o, inv);
-            // te == inf is a miss; it must not pass when best is inf too (open floor)
-            const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f;
-            if (enter && nd.leaf >= 0) {
-                const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
-                if (COUNT) c_tests += (uint32_t)cnt;
-                for (int k2 = 0; k2 < cnt; ++k2) {
-                    const BvhSphere sp = kp.bvh_prims[first + k2];
-                    const float t = sphere_t(sp.r, o - v3(sp.c[0], sp.c[1], sp.c[2]), d);
-                    if (isfinite_(t) && gt_1em6(fabs_(t)) &&
-                        (t < best || (t == best && bidx >= 0 && sp.index < bidx))) {
-                        best = t;
-                        bidx = sp.index;
-                    }
-                }
-                i = nd.skip;
-            } else {
-                i = enter ? i + 1 : nd.skip;
-            }
-        }
+        sphere_bvh_walk<COUNT>(kp, o, d, i, best, bidx, 0x7fffffff, c_nodes, c_tests);
     } else {
         if (COUNT) c_tests += (uint32_t)kp.n_spheres;
         for (int i = 0; i < kp.n_spheres; ++i) {
@@ -373,8 +389,13 @@ struct LightSet {
 
 // GEOM (IPT_GEOM_*) is a template parameter so that the box instance carries
 // neither the sphere-list code nor its pointers (SGPR pressure).
+// Sphere-list instances carry the resumable walk's state (IPT_RESUME): they
+// are given 3 waves per SIMD of registers (their LDS allows 3 workgroups).
+__host__ __device__ constexpr int waves_per_simd(int geom) {
+    return (IPT_RESUME && (geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES)) ? 3 : IPT_WAVES_PER_SIMD;
+}
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
-__global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const KParams kp) {
+__global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(const KParams kp) {
     constexpr int kFrameSlots = frame_slots(GEOM);
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
@@ -442,6 +463,16 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
     Win8 w;
     vec3 tpos = v3(0, 0, 0);
     int fdepth = -1;  // depth of the sphere node whose frame is in the lane's column
+    // Resumable sphere-BVH walks (sphere-list scenes): a lane whose walk is not
+    // done within IPT_WALK_BUDGET node visits keeps its ray and light results
+    // and resumes the walk in the next steps (doing nothing else meanwhile), so
+    // a step costs the budget, not the longest walk of the workgroup.
+    constexpr bool kRes = IPT_RESUME && (GEOM == IPT_GEOM_SPHERES_IN_BOX || GEOM == IPT_GEOM_SPHERES);
+    bool tracing = false;
+    vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
+    int xrdepth = 0, xi = 0, xbidx = -1, xp = -1;
+    bool xis_iter = false, xhas_li = false;
+    float xmult = 0.0f, xli_pow = 0.0f, xbest = 0.0f;
     float tres = 0.0f;
     int ti = 0, tdepth = 0, tkind = 0;  // kind: 0..4 wall plane, 5 box sphere, 6+i extra sphere i
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
@@ -496,7 +527,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         IPT_STAMP_AT(1);  // refill
         if (active) { IPT_PHASE(0); }
         // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
-        if (active && has_path && !fresh) {
+        if (active && has_path && !fresh && !(kRes && tracing)) {
             for (;;) {
                 const int n = kp.n_rays >> tdepth;
                 if (ti < n) break;
@@ -532,7 +563,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         // workgroup (RotateDdf frames of sphere nodes, CosineDdf local samples) so
         // that they run on ceil(N/64) dense wave-passes instead of on every wave.
         const int par = step & 1;
-        bool want_frame = need_frame && has_path && !fresh;
+        bool want_frame = need_frame && has_path && !fresh && !(kRes && tracing);
         int slot_f = 0;
         {
             const uint64_t m = __ballot(want_frame);
@@ -562,7 +593,7 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
             xfr[3 * kFrameSlots + slot_f] = __int_as_float(tid);
         }
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
-        const bool iter_lane = active && has_path && !fresh && !stalled;
+        const bool iter_lane = active && has_path && !fresh && !stalled && !(kRes && tracing);
         int pick = -1;
         float u1 = 0.0f, u2 = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
         if (iter_lane) {
@@ -759,6 +790,64 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
         ++step;
         IPT_STAMP_AT(8);  // direction
         // --------------------------------------------- phase 4: trace + resolve
+        // the child's value (main.cpp:100-143) from its traces, then push it,
+        // add it to the current node's sum, or finish the path
+        auto resolve = [&](bool traced, float t, int prim, vec3 o, vec3 d, int depth, bool iter, float mult,
+                           bool has_li, vec3 li_pos, float li_pow) {
+            float cv = 0.0f;
+            bool push = false;
+            vec3 si_pos = v3(0, 0, 0);
+            if (traced) {
+                const bool has_si = prim >= 0;
+                if (COUNT) {
+                    ++c_traced;
+                    c_surf += has_si ? 1u : 0u;
+                    c_light += has_li ? 1u : 0u;
+                }
+                if (has_si) si_pos = o + d * t;
+                if (has_li && (!has_si || longer(si_pos - o, li_pos - o))) {
+                    cv = isfinite_(li_pow) ? li_pow : 1.0f;
+                } else if (!has_si) {
+                    cv = 0.0f;
+                } else {
+                    if (COUNT) ++c_exp;
+                    const int nchild = kp.n_rays >> depth;
+                    if (nchild == 0) {
+                        const float zero = 0.0f;
+                        cv = zero / (float)nchild;  // 0/0: the NaN that poisons the parent
+                    } else {
+                        push = true;
+                    }
+                }
+            }
+            if (push) {
+                IPT_PHASE(10);
+                if (iter) {
+                    float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
+                    b[0 * kBlock] = tpos.x;
+                    b[1 * kBlock] = tpos.y;
+                    b[2 * kBlock] = tpos.z;
+                    b[3 * kBlock] = tres;
+                    b[4 * kBlock] = mult;
+                    b[5 * kBlock] = __int_as_float(ti | (tkind << 8));
+                }
+                tpos = si_pos;
+                tkind = prim;
+                if (prim >= 5) {
+                    need_frame = true;  // built by the frame pass of the next step
+                    if (COUNT) ++c_sframe;
+                }
+                tres = 0.0f;
+                ti = 0;
+                tdepth = depth;
+            } else if (iter) {
+                tres = tres + (mult * 1.0f) * cv;
+            } else {
+                // the camera ray itself ended (light, miss, depth_max or n_rays==0)
+                kp.values[unit] = cv >= 0.0f ? cv : 0.0f;
+                has_path = false;
+            }
+        };
         if (have_ray) {
             IPT_PHASE(8);
             // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
@@ -816,68 +905,48 @@ __global__ __launch_bounds__(kBlock, IPT_WAVES_PER_SIMD) void path_kernel(const 
                 const float mix = lmix + w_sdf * sdf_val;
                 mult = div_(sdf_val, mix);
             }
-            // child ray_power (main.cpp:100-143)
-            float cv = 0.0f;
-            bool push = false;
-            vec3 si_pos = v3(0, 0, 0);
-            int prim = -1;
-            if (rdepth < kp.depth_max) {
-                IPT_PHASE(9);
-                const float t = trace_geometry<COUNT, GEOM>(kp, ro, rd, &prim, c_nodes, c_tests);
-                if (IPT_ABL == 5) {
-                    int p2;
-                    keep_alive(trace_geometry<false, GEOM>(kp, ro, rd * (1.0f + kp.abl_zero), &p2, c_nodes, c_tests));
-                    keep_alive(p2);
-                }
-                IPT_STAMP_AT(10);  // mixture value + geometry trace
-                const bool has_si = prim >= 0;
-                if (COUNT) {
-                    ++c_traced;
-                    c_surf += has_si ? 1u : 0u;
-                    c_light += has_li ? 1u : 0u;
-                }
-                if (has_si) si_pos = ro + rd * t;
-                if (has_li && (!has_si || longer(si_pos - ro, li_pos - ro))) {
-                    cv = isfinite_(li_pow) ? li_pow : 1.0f;
-                } else if (!has_si) {
-                    cv = 0.0f;
-                } else {
-                    if (COUNT) ++c_exp;
-                    const int nchild = kp.n_rays >> rdepth;
-                    if (nchild == 0) {
-                        const float zero = 0.0f;
-                        cv = zero / (float)nchild;  // 0/0: the NaN that poisons the parent
-                    } else {
-                        push = true;
-                    }
-                }
-            }
-            if (push) {
-                IPT_PHASE(10);
-                if (is_iter) {
-                    float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
-                    b[0 * kBlock] = tpos.x;
-                    b[1 * kBlock] = tpos.y;
-                    b[2 * kBlock] = tpos.z;
-                    b[3 * kBlock] = tres;
-                    b[4 * kBlock] = mult;
-                    b[5 * kBlock] = __int_as_float(ti | (tkind << 8));
-                }
-                tpos = si_pos;
-                tkind = prim;
-                if (prim >= 5) {
-                    need_frame = true;  // built by the frame pass of the next step
-                    if (COUNT) ++c_sframe;
-                }
-                tres = 0.0f;
-                ti = 0;
-                tdepth = rdepth;
-            } else if (is_iter) {
-                tres = tres + (mult * 1.0f) * cv;
+            // child ray_power (main.cpp:100-143): the geometry trace, then resolve
+            if (kRes && rdepth < kp.depth_max && kp.n_nodes > 0) {
+                // resumable walk: keep the ray and the light results, planes now
+                xro = ro;
+                xrd = rd;
+                xrdepth = rdepth;
+                xis_iter = is_iter;
+                xmult = mult;
+                xhas_li = has_li;
+                xli_pos = li_pos;
+                xli_pow = li_pow;
+                xp = -1;
+                xbidx = -1;
+                xi = 0;
+                xbest = inf_();
+                if (GEOM == IPT_GEOM_SPHERES_IN_BOX)
+                    xbest = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(ro, rd, &xp)
+                                                           : trace_box_planes_only<false>(ro, rd, &xp);
+                tracing = true;
             } else {
-                // the camera ray itself ended (light, miss, depth_max or n_rays==0)
-                kp.values[unit] = cv >= 0.0f ? cv : 0.0f;
-                has_path = false;
+                int prim = -1;
+                float t = inf_();
+                if (rdepth < kp.depth_max) {
+                    IPT_PHASE(9);
+                    t = trace_geometry<COUNT, GEOM>(kp, ro, rd, &prim, c_nodes, c_tests);
+                    if (IPT_ABL == 5) {
+                        int p2;
+                        keep_alive(trace_geometry<false, GEOM>(kp, ro, rd * (1.0f + kp.abl_zero), &p2, c_nodes, c_tests));
+                        keep_alive(p2);
+                    }
+                    IPT_STAMP_AT(10);  // mixture value + geometry trace
+                }
+                resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
+            }
+        }
+        if (kRes && tracing) {
+            IPT_PHASE(9);
+            sphere_bvh_walk<COUNT>(kp, xro, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
+            if (xi >= kp.n_nodes) {
+                tracing = false;
+                resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : xp, xro, xrd, xrdepth, xis_iter, xmult, xhas_li, xli_pos,
+                        xli_pow);
             }
         }
     }
