@@ -59,6 +59,9 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_WALK_BUDGET
 #define IPT_WALK_BUDGET 48  // node visits per lane per step of a resumable walk
 #endif
+#ifndef IPT_WHILE_WHILE
+#define IPT_WHILE_WHILE 1  // BVH walks as while-while loops (leaf work outside the node loop)
+#endif
 #ifndef IPT_LENCMP
 #define IPT_LENCMP 1  // length(a) > length(b) decided on the squares when they are far apart
 #endif
@@ -223,6 +226,41 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
     // near-child-first linearisation for this direction octant (ipt_bvh.h)
     const int oct = (int)(f2u(d.x) >> 31) | (int)(f2u(d.y) >> 31) << 1 | (int)(f2u(d.z) >> 31) << 2;
     const BvhNode* __restrict__ nodes = kp.bvh_nodes + (size_t)oct * kp.n_nodes;
+#if IPT_WHILE_WHILE
+    // while-while (Aila & Laine 2009): the inner loop only walks nodes until
+    // each lane stands on an entered leaf (or is done), so the leaf's sphere
+    // tests run with all such lanes together instead of once per wave-iteration
+    while (i < kp.n_nodes && budget > 0) {
+        int leaf = -1;
+        while (i < kp.n_nodes && budget > 0) {
+            --budget;
+            const BvhNode nd = nodes[i];
+            if (COUNT) ++c_nodes;
+            const float te = bvh_box_entry(nd, o, inv);
+            // te == inf is a miss; it must not pass when best is inf too (open floor)
+            const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f;
+            if (enter && nd.leaf >= 0) {
+                leaf = nd.leaf;
+                i = nd.skip;
+                break;
+            }
+            i = enter ? i + 1 : nd.skip;
+        }
+        if (leaf >= 0) {
+            const int first = leaf & 0xffffff, cnt = leaf >> 24;
+            if (COUNT) c_tests += (uint32_t)cnt;
+            for (int k2 = 0; k2 < cnt; ++k2) {
+                const BvhSphere sp = kp.bvh_prims[first + k2];
+                const float t = sphere_t(sp.r, o - v3(sp.c[0], sp.c[1], sp.c[2]), d);
+                if (isfinite_(t) && gt_1em6(fabs_(t)) &&
+                    (t < best || (t == best && bidx >= 0 && sp.index < bidx))) {
+                    best = t;
+                    bidx = sp.index;
+                }
+            }
+        }
+    }
+#else
     while (i < kp.n_nodes && budget-- > 0) {
         const BvhNode nd = nodes[i];
         if (COUNT) ++c_nodes;
@@ -246,6 +284,7 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
             i = enter ? i + 1 : nd.skip;
         }
     }
+#endif
 }
 
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
@@ -336,7 +375,7 @@ constexpr int kLdsCand = 512;
 // the box scene makes ~25 per step, the sphere-list scene (nearly every hit a
 // sphere) well over 64
 __host__ __device__ constexpr int frame_slots(int geom) {
-    return geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES || geom == IPT_GEOM_SMALLPT ? 256 : 64;
+    return geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES || geom == IPT_GEOM_SMALLPT ? kBlock : kBlock / 4;
 }
 // LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
 // task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
@@ -881,6 +920,28 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 // a skipped light would add +0 to lmix and never be nearest
                 const vec3 inv = v3(safe_rcp(rd.x), safe_rcp(rd.y), safe_rcp(rd.z));
                 int i = 0;
+#if IPT_WHILE_WHILE
+                // while-while: walk to the next entered leaf, then run the
+                // leaf's light steps with every lane that stands on one
+                while (i < kp.n_light_nodes) {
+                    int leaf = -1;
+                    while (i < kp.n_light_nodes) {
+                        const BvhNode nd = kp.light_nodes[i];
+                        if (COUNT) ++c_lnode;
+                        const bool enter = bvh_box_entry(nd, ro, inv) != inf_();
+                        if (enter && nd.leaf >= 0) {
+                            leaf = nd.leaf;
+                            i = nd.skip;
+                            break;
+                        }
+                        i = enter ? i + 1 : nd.skip;
+                    }
+                    if (leaf >= 0) {
+                        const int first = leaf & 0xffffff, cnt = leaf >> 24;
+                        for (int l = first; l < first + cnt; ++l) light_step(l);
+                    }
+                }
+#else
                 while (i < kp.n_light_nodes) {
                     const BvhNode nd = kp.light_nodes[i];
                     if (COUNT) ++c_lnode;
@@ -893,6 +954,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                         i = enter ? i + 1 : nd.skip;
                     }
                 }
+#endif
             } else {
                 for (int l = 0; l < nl; ++l) light_step(l);
             }
