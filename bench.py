@@ -136,12 +136,27 @@ def main():
         if rank == 0:
             print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
     dist = None
+    # IPT_BENCH_SHARE_GPU=1 (rehearsal only): every rank on cuda:0, frame-end
+    # collectives over gloo on host copies, so the N>1 path runs on a 1-GPU box
+    share = os.environ.get("IPT_BENCH_SHARE_GPU") == "1"
+    if share:
+        local_rank = 0
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+
+    def coll(fn, t, *a, **kw):  # collective on a device tensor (host copy under gloo)
+        if not share:
+            return fn(t, *a, **kw)
+        h = t.cpu()
+        fn(h, *a, **kw)
+        t.copy_(h)
 
     from ipt_amd import capi, roofline, scenes
 
@@ -188,10 +203,10 @@ def main():
     if dist:
         # frame end: assemble the GridRenderPlane on rank 0 (each pixel is owned
         # by exactly one rank, the others hold zeros)
-        dist.reduce(pixels, 0, op=dist.ReduceOp.SUM)
-        dist.reduce(counters, 0, op=dist.ReduceOp.SUM)
-        dist.reduce(sums, 0, op=dist.ReduceOp.SUM)
-        dist.reduce(pmax, 0, op=dist.ReduceOp.MAX)
+        coll(dist.reduce, pixels, 0, op=dist.ReduceOp.SUM)
+        coll(dist.reduce, counters, 0, op=dist.ReduceOp.SUM)
+        coll(dist.reduce, sums, 0, op=dist.ReduceOp.SUM)
+        coll(dist.reduce, pmax, 0, op=dist.ReduceOp.MAX)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -199,7 +214,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         tt = torch.tensor([elapsed, path_ms, acc_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        coll(dist.all_reduce, tt, op=dist.ReduceOp.MAX)
         elapsed, path_ms, acc_ms = tt.tolist()
 
     spp_total = args.steps * args.spp_per_step
@@ -221,7 +236,7 @@ def main():
             t.copy_(s)
         if dist:
             ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64, device=dev)
-            dist.all_reduce(ct)
+            coll(dist.all_reduce, ct)
             cnt = dict(zip(capi.COUNTER_NAMES, [int(x) for x in ct.tolist()]))
         ops = roofline.ops_from_counters(cnt, n_spheres=len(desc.get("spheres", [])))
         # per launch on one rank: ops/world per launch, average launch duration
@@ -232,6 +247,8 @@ def main():
         acc_launch_s = acc_ms / 1e3 / args.steps
         traffic = None
         traffic_src = None
+        cos_samples = cnt["iterations"] - cnt["light_samples"]
+        path_alg_bytes = roofline.path_bytes(total_paths // world // args.steps, cos_samples // world // args.steps)
         pmc_file = ROOT / "profiles" / "pmc_latest.json"
         if pmc_file.exists():
             try:
@@ -265,8 +282,21 @@ def main():
             "launch_ms": launch_s * 1e3,
             "note": ("algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
                      "counters) per launch / HIP-event launch time; VALU issue peak "
-                     "256CU x 4 SIMD32 x 2.4GHz; path kernel compulsory HBM is 5 B/path"),
+                     "256CU x 4 SIMD32 x 2.4GHz; 'hbm': the path kernel's HBM side "
+                     "(algorithmic bytes: 5 B radiance+code per path + 16 B of CosineDdf "
+                     "table gathers per cosine-sampled iteration; 'measured' = rocprofv3 "
+                     "FETCH_SIZE+WRITE_SIZE of the same config, random 8-byte gathers "
+                     "fetch whole lines)"),
             "hbm": {
+                "kernel": "path_kernel",
+                "achieved": path_alg_bytes / launch_s / 1e9,
+                "measured": (traffic / launch_s / 1e9) if traffic else None,
+                "peak": roofline.HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": path_alg_bytes / launch_s / 1e9 / roofline.HBM_PEAK_GBPS,
+                "bytes_per_path": path_alg_bytes / (total_paths // world // args.steps),
+            },
+            "hbm_accumulate": {
                 "kernel": "accumulate_kernel",
                 "bound": "hbm",
                 "achieved": acc_bytes / acc_launch_s / 1e9 if acc_launch_s > 0 else None,
@@ -275,7 +305,6 @@ def main():
                 "frac": (acc_bytes / acc_launch_s / 1e9 / roofline.HBM_PEAK_GBPS
                          if acc_launch_s > 0 else None),
                 "launch_ms": acc_launch_s * 1e3,
-                "path_kernel_algorithmic_GBps": roofline.path_bytes(total_paths // world // args.steps) / launch_s / 1e9,
             },
         }
 

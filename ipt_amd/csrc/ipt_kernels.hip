@@ -142,7 +142,7 @@ struct KParams {
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
     int box_inrange;                      // camera and sphere list within 2^39 (box_plane_t<true>)
-    const float2* __restrict__ cos_a;     // [2^24] CosineDdf table by u1's 24 bits: (cos_alpha, sin(alpha))
+    const float* __restrict__ cos_a;      // [2^24] CosineDdf table by u1's 24 bits: sin(acos(sqrt(u1)))
     const float2* __restrict__ cos_b;     // [2^24] by u2's 24 bits: (cos phi, sin phi)
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
@@ -674,14 +674,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 u1 = u01(r1);
                 u2 = u01(r2);
                 if (c == nl) {
-                    // CosineDdf::sample (ddf.cpp:223-231) of (u1, u2) = (cos_alpha, r) x
+                    // CosineDdf::sample (ddf.cpp:223-231) of (u1, u2): (cos_alpha, r) x
                     // (cos phi, sin phi) looked up by the draws' 24 bits; consumed after
                     // barrier B, so the loads' latency hides behind the frame pass
                     // (a non-temporal hint measured slower on C2 and C5)
-                    const float2 ta = kp.cos_a[r1 >> 8];
+                    // (cos_alpha = sqrtf(u1) is recomputed in the direction phase:
+                    // the 64 MiB r table + the 128 MiB phi table gather less)
+                    const float tr = kp.cos_a[r1 >> 8];
                     const float2 tb = kp.cos_b[r2 >> 8];
-                    u1 = ta.x;
-                    u2 = ta.y;
+                    u2 = tr;
                     cs_c = tb.x;
                     cs_s = tb.y;
                 }
@@ -812,7 +813,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
                 fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
                 // cosine_sample_local from the tables: (r cos phi, r sin phi, cos_alpha)
-                dir = frame_apply(fm, v3(u2 * cs_c, u2 * cs_s, u1));
+                // with u2 = r and cos_alpha = sqrtf(u1)
+                dir = frame_apply(fm, v3(u2 * cs_c, u2 * cs_s, sqrt_(u1)));
             }
             ++ti;
             if (COUNT) ++c_iter;
@@ -1169,7 +1171,7 @@ __global__ void math_kernel(int fn, const float* in, float* out, long long n) {
 __global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ params, const LightDev* __restrict__ lights,
                            const float* __restrict__ weights, const float* __restrict__ cdf, int nl,
                            const float* __restrict__ in, long long n, float* __restrict__ out,
-                           const float2* __restrict__ cos_a, const float2* __restrict__ cos_b) {
+                           const float* __restrict__ cos_a, const float2* __restrict__ cos_b) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const vec3 o = v3(params[0], params[1], params[2]);
@@ -1181,8 +1183,9 @@ __global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ p
             v = frame_apply(make_frame(o), cosine_sample_local(u1, u2));
         } else if (kind == 3) {
             // the path kernel's table lookup (u on the RNG's 2^-24 grid, checked by the caller)
-            const float2 ta = cos_a[(uint32_t)(u1 * 16777216.0f)], tb = cos_b[(uint32_t)(u2 * 16777216.0f)];
-            v = frame_apply(make_frame(o), v3(ta.y * tb.x, ta.y * tb.y, ta.x));
+            const float tr = cos_a[(uint32_t)(u1 * 16777216.0f)];
+            const float2 tb = cos_b[(uint32_t)(u2 * 16777216.0f)];
+            v = frame_apply(make_frame(o), v3(tr * tb.x, tr * tb.y, sqrt_(u1)));
         } else if (kind == 1) {
             v = light_sample_dir(lights[(int)params[3]], o, u1, u2);
         } else {
@@ -1218,11 +1221,11 @@ __global__ void ddf_kernel(int value_mode, int kind, const float* __restrict__ p
 }
 
 // Exact CosineDdf tables (ddf.cpp:223-231) over the 2^24 values a draw can
-// take (u = i * 2^-24, ipt_math.h u01): a[i] = (sqrtf(u), sinf(acosf(sqrtf(u)))),
-// b[i] = sincosf((float)(2*M_PI*u)) as (cos, sin). cosine_sample_local(u1, u2)
-// == (a[i1].y*b[i2].x, a[i1].y*b[i2].y, a[i1].x) bit for bit (same functions,
-// same products).
-__global__ void cos_table_kernel(float2* __restrict__ a, float2* __restrict__ b) {
+// take (u = i * 2^-24, ipt_math.h u01): a[i] = sinf(acosf(sqrtf(u))) (64 MiB),
+// b[i] = sincosf((float)(2*M_PI*u)) as (cos, sin) (128 MiB).
+// cosine_sample_local(u1, u2) == (a[i1]*b[i2].x, a[i1]*b[i2].y, sqrtf(u1)) bit
+// for bit (same functions, same products).
+__global__ void cos_table_kernel(float* __restrict__ a, float2* __restrict__ b) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (1u << 24)) return;
     const float u = u01(i << 8);
@@ -1230,7 +1233,7 @@ __global__ void cos_table_kernel(float2* __restrict__ a, float2* __restrict__ b)
     const float r = sinf_small_(acosf_(cos_alpha));
     float sp, cp;
     sincosf_small_(two_pi_times(u), &sp, &cp);
-    a[i] = make_float2(cos_alpha, r);
+    a[i] = r;
     b[i] = make_float2(cp, sp);
 }
 
@@ -1300,7 +1303,8 @@ struct ipt_ctx {
     int cand_cap_rows = 0, cand_cap_h = 0;
     unsigned long long* d_unit = nullptr;
     unsigned long long* d_counters = nullptr;
-    float2* d_cos_a = nullptr;  // CosineDdf tables (cos_table_kernel), 2 x 128 MiB
+    float* d_cos_a = nullptr;   // CosineDdf tables (cos_table_kernel): r 64 MiB,
+                                // (cos phi, sin phi) 128 MiB
     float2* d_cos_b = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
@@ -1328,7 +1332,7 @@ int fail(ipt_ctx* ctx, int code, const std::string& msg) {
 int ensure_cos_tables(ipt_ctx* ctx, hipStream_t st) {
     if (ctx->d_cos_a) return IPT_OK;
     const size_t n = (size_t)1 << 24;
-    HIPCHECK(ctx, hipMalloc(&ctx->d_cos_a, n * sizeof(float2)));
+    HIPCHECK(ctx, hipMalloc(&ctx->d_cos_a, n * sizeof(float)));
     HIPCHECK(ctx, hipMalloc(&ctx->d_cos_b, n * sizeof(float2)));
     hipLaunchKernelGGL(cos_table_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, st, ctx->d_cos_a, ctx->d_cos_b);
     HIPCHECK(ctx, hipGetLastError());
