@@ -137,6 +137,7 @@ struct KParams {
     int n_nodes;
     const BvhNode* __restrict__ light_nodes;   // n_light_nodes > 0: light BVH over index ranges
     int n_light_nodes;
+    int lnodes_lds;                       // light BVH staged in LDS (kLightsGlobal)
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
@@ -388,6 +389,14 @@ __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
     return 12 * (size_t)kFrameStride + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) +
            4 + 4 * (size_t)frame_slots(geom);
 }
+// kLightsGlobal: mixture weights + CDF (and, when small, the light BVH) are
+// staged in LDS after the fixed layout: their global copies would be evicted
+// from L2 by the CosineDdf gathers, and the pick / walk are chains of
+// dependent loads.
+constexpr int kLdsLightNodesMax = 512;
+__host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds) {
+    return (size_t)((2 * (nl + 1) + 3) & ~3) + 8 * (size_t)n_nodes_lds;
+}
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4
 #endif
@@ -416,12 +425,12 @@ struct LightSet {
     }
     __device__ __forceinline__ float weight(int i) const {
         if (LMODE == kLightsOne) return w0;
-        if (LMODE == kLightsLds) return wl[i];
+        if (LMODE == kLightsLds || LMODE == kLightsGlobal) return wl[i];
         return wg[i];
     }
     __device__ __forceinline__ float cdf(int i) const {
         if (LMODE == kLightsOne) return i == 0 ? c0 : c1;
-        if (LMODE == kLightsLds) return cl[i];
+        if (LMODE == kLightsLds || LMODE == kLightsGlobal) return cl[i];
         return cg[i];
     }
 };
@@ -446,6 +455,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                                        (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
     float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [4][kFrameSlots] frame tasks: normal, lane
     int* cand_lds = reinterpret_cast<int*>(xfr + 4 * kFrameSlots);  // [kLdsCand] when kp.cand_lds
+    // kLightsGlobal: [weights | cdf | light BVH nodes] after the candidate rows
+    float* gl_lds = reinterpret_cast<float*>(cand_lds) + (kp.cand_lds ? kLdsCand : 0);
+    BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + ((2 * (kp.n_lights + 1) + 3) & ~3));
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     if (tid < 4) xcnt[tid] = 0;
@@ -463,12 +475,23 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
     }
     if (cand_in_lds)
         for (int i = tid; i < kp.n_cand; i += kBlock) cand_lds[i] = kp.cand_rows[i];
+    if (LMODE == kLightsGlobal) {
+        for (int i = tid; i <= kp.n_lights; i += kBlock) {
+            gl_lds[i] = kp.weights[i];
+            gl_lds[kp.n_lights + 1 + i] = kp.cdf[i];
+        }
+        if (kp.lnodes_lds) {
+            const float4* src = reinterpret_cast<const float4*>(kp.light_nodes);
+            float4* dst = reinterpret_cast<float4*>(lnodes_lds);
+            for (int i = tid; i < 2 * kp.n_light_nodes; i += kBlock) dst[i] = src[i];
+        }
+    }
     __syncthreads();
     LightSet<LMODE> LS;
     LS.lds = lights_lds;
     LS.glob = kp.lights;
-    LS.wl = weights_lds;
-    LS.cl = cdf_lds;
+    LS.wl = LMODE == kLightsGlobal ? gl_lds : weights_lds;
+    LS.cl = LMODE == kLightsGlobal ? gl_lds + kp.n_lights + 1 : cdf_lds;
     LS.wg = kp.weights;
     LS.cg = kp.cdf;
     if (LMODE == kLightsOne) {
@@ -921,6 +944,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 // index-ordered light BVH (ipt_bvh.h): lights met in scan order;
                 // a skipped light would add +0 to lmix and never be nearest
                 const vec3 inv = v3(safe_rcp(rd.x), safe_rcp(rd.y), safe_rcp(rd.z));
+                auto walk = [&](const BvhNode* __restrict__ lnodes) {
                 int i = 0;
 #if IPT_WHILE_WHILE
                 // while-while: walk to the next entered leaf, then run the
@@ -928,7 +952,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 while (i < kp.n_light_nodes) {
                     int leaf = -1;
                     while (i < kp.n_light_nodes) {
-                        const BvhNode nd = kp.light_nodes[i];
+                        const BvhNode nd = lnodes[i];
                         if (COUNT) ++c_lnode;
                         const bool enter = bvh_box_entry(nd, ro, inv) != inf_();
                         if (enter && nd.leaf >= 0) {
@@ -945,7 +969,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 }
 #else
                 while (i < kp.n_light_nodes) {
-                    const BvhNode nd = kp.light_nodes[i];
+                    const BvhNode nd = lnodes[i];
                     if (COUNT) ++c_lnode;
                     const bool enter = bvh_box_entry(nd, ro, inv) != inf_();
                     if (enter && nd.leaf >= 0) {
@@ -957,6 +981,11 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                     }
                 }
 #endif
+                };
+                if (kp.lnodes_lds)
+                    walk(lnodes_lds);
+                else
+                    walk(kp.light_nodes);
             } else {
                 for (int l = 0; l < nl; ++l) light_step(l);
             }
@@ -1290,6 +1319,7 @@ struct ipt_ctx {
     int cdf_bsearch = 0;
     bool any_round_light = false;
     int bpc_override = 0;
+    int lnodes_lds = 0;  // IPT_LNODES_LDS=1: stage the light BVH in LDS
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int box_inrange = 0;
     // work buffers
@@ -1421,7 +1451,9 @@ int needed_susp(const ipt_params* p) {
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
-                        (kp.cand_lds ? kLdsCand : 0)) * sizeof(float);
+                        (kp.cand_lds ? kLdsCand : 0) +
+                        (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0)
+                                                : 0)) * sizeof(float);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // persistent grid: every block the CUs can hold at once (a work queue, no
@@ -1538,6 +1570,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.n_nodes = ctx->n_nodes;
         kp.light_nodes = ctx->d_light_nodes;
         kp.n_light_nodes = ctx->n_light_nodes;
+        // light BVH staged in LDS only on request (IPT_LNODES_LDS=1 at ipt_create):
+        // measured, the lost fourth workgroup per CU costs more (C5 25.5 vs 26.3)
+        kp.lnodes_lds = (ctx->lnodes_lds && ctx->n_light_nodes > 0 && ctx->n_light_nodes <= kLdsLightNodesMax) ? 1 : 0;
         kp.cdf_bsearch = ctx->cdf_bsearch;
         kp.cos_a = ctx->d_cos_a;
         kp.cos_b = ctx->d_cos_b;
@@ -1627,6 +1662,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     ctx->device = hip_device;
     ctx->n_cu = prop.multiProcessorCount;
     if (const char* e = std::getenv("IPT_BLOCKS_PER_CU")) ctx->bpc_override = std::atoi(e);  // profiling only
+    if (const char* e = std::getenv("IPT_LNODES_LDS")) ctx->lnodes_lds = std::atoi(e) != 0;
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return fail(nullptr, IPT_E_DEVICE, "stream creation failed");

@@ -261,3 +261,20 @@ def test_spheres_in_box_bit_exact(gpu_ctx, oracle, n):
     gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
     assert np.array_equal(gc, oc)
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+@pytest.mark.parametrize("desc_fn", [lambda: scenes.make_scene_box_lights(16),
+                                     lambda: scenes.make_scene_random_lights(300, seed=7)])
+def test_light_bvh_in_lds_bit_exact(oracle, monkeypatch, desc_fn):
+    """The optional LDS-staged light BVH (IPT_LNODES_LDS=1, read at ipt_create)
+    walks the same nodes as the global-memory copy: bit-exact vs the oracle."""
+    monkeypatch.setenv("IPT_LNODES_LDS", "1")
+    ctx = capi.Context(0)
+    try:
+        desc = desc_fn()
+        p = capi.make_params(20, 16, 2, n_rays=8, depth_max=6)
+        gv, gc, ov, oc = _render_both(ctx, desc, p, oracle)
+        assert np.array_equal(gc, oc)
+        assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+    finally:
+        ctx.close()
