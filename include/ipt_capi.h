@@ -248,7 +248,10 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
    fn: 0 acosf, 1 sinf, 2 cosf, 3 (float)acos((double)x), 4 sincosf->sin,
        5 sincosf->cos, 6 sqrtf, 7 CosineDdf z/M_PI, 8 (float)(2*M_PI*u),
        9 a/b over the division pairs of the fast-division proof (x's bit
-         pattern -> an in-range numerator and hashed denominator)            */
+         pattern -> an in-range numerator and hashed denominator),
+      10 the range-free division (box planes) over the same pairs,
+      11 the squares-first length comparison over near-tie pairs (0/1),
+      12 the 32-bit work-unit division over hashed (n, d) pairs (bit pattern) */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
 /* Device self-check of the fast math paths: for every float bit pattern b in

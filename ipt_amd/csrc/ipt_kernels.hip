@@ -152,7 +152,7 @@ struct KParams {
 // error is below (n/d) * 2^-51 < 1/d (n < 2^32), i.e. below the distance of a
 // non-integer n/d from the next integer, so it truncates to the quotient or,
 // when n/d is an integer approached from below, to one less (fixed up).
-__device__ __forceinline__ uint32_t udiv_exact(uint32_t n, uint32_t d, double inv_d) {
+__host__ __device__ inline uint32_t udiv_exact(uint32_t n, uint32_t d, double inv_d) {
     uint32_t q = (uint32_t)((double)n * inv_d);
     if (n - q * d >= d) ++q;
     return q;
@@ -161,8 +161,7 @@ __device__ __forceinline__ uint32_t udiv_exact(uint32_t n, uint32_t d, double in
 // a, b with squares x, y: sqrtf is monotone, so x <= y gives false, and
 // x > y(1+2^-20) (y normal) separates the two correctly rounded roots by more
 // than their rounding; only the rare near-ties (or NaN/tiny) take the roots.
-__device__ __forceinline__ bool longer(vec3 a, vec3 b) {
-    const float x = dot(a, a), y = dot(b, b);
+__device__ __forceinline__ bool longer_sq(float x, float y) {
     if (!IPT_LENCMP) return sqrt_(x) > sqrt_(y);
     const bool far_gt = x > y * 1.000001907f && y >= 1e-30f;  // 1 + 2^-19
     const bool le = x <= y;
@@ -172,6 +171,7 @@ __device__ __forceinline__ bool longer(vec3 a, vec3 b) {
         if (tie) r = sqrt_(x) > sqrt_(y);
     return r;
 }
+__device__ __forceinline__ bool longer(vec3 a, vec3 b) { return longer_sq(dot(a, a), dot(b, b)); }
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
     if (kp.n_shards <= 1 || kp.tile_rows <= 0) return true;
@@ -1172,8 +1172,43 @@ __device__ __host__ inline float div_pair_b(uint32_t b) {
     return u2f((h & 0x807fffffu) | ((87u + ((h >> 23) & 0xffu) % 81u) << 23));
 }
 
+// fn 11 / 12 probes: a 32-bit pattern b seeds a pair.
+//  11: x = |b| as a float, y = x moved by a hashed -64..63 ulps (every 16th
+//      pair: an unrelated hashed float) -> longer_sq(x, y) as 0/1;
+//  12: n = b, d = a hashed divisor of hashed magnitude -> udiv_exact(n, d).
+__device__ __host__ inline uint32_t probe_hash(uint32_t b) {
+    uint32_t h = b * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    return h;
+}
+__device__ __host__ inline void longer_pair(uint32_t b, float* x, float* y) {
+    const uint32_t h = probe_hash(b);
+    const uint32_t xb = b & 0x7fffffffu;
+    *x = u2f(xb);
+    *y = (h & 15u) == 0u ? u2f(probe_hash(h) & 0x7fffffffu) : u2f(xb + ((h >> 4) & 127u) - 64u);
+}
+__device__ __host__ inline uint32_t udiv_pair_d(uint32_t b) {
+    const uint32_t h = probe_hash(b ^ 0x5bd1e995u);
+    return (h >> (h & 31u)) | 1u;
+}
 __device__ __host__ inline float math_fn(int fn, float x) {
     switch (fn) {
+        case 10: return div_inrange_(div_pair_a(f2u(x)), div_pair_b(f2u(x)));
+        case 11: {
+            float a, b;
+            longer_pair(f2u(x), &a, &b);
+#if defined(__HIP_DEVICE_COMPILE__)
+            return longer_sq(a, b) ? 1.0f : 0.0f;
+#else
+            return sqrt_(a) > sqrt_(b) ? 1.0f : 0.0f;
+#endif
+        }
+        case 12: {
+            const uint32_t d = udiv_pair_d(f2u(x));
+            return u2f(udiv_exact(f2u(x), d, 1.0 / (double)d));
+        }
         case 0: return acosf_(x);
         case 1: return sinf_(x);
         case 2: return cosf_(x);
@@ -1271,7 +1306,13 @@ __global__ void cos_table_kernel(float* __restrict__ a, float2* __restrict__ b) 
 __device__ float math_fn_exact(int fn, float x) {
     if (fn == 3) return acos_f64_to_f32_exact(x);
     if (fn == 6) return __builtin_sqrtf(x);                                      // IEEE (compiler sequence)
-    if (fn == 9) return div_pair_a(f2u(x)) / div_pair_b(f2u(x));                // IEEE (compiler sequence)
+    if (fn == 9 || fn == 10) return div_pair_a(f2u(x)) / div_pair_b(f2u(x));   // IEEE (compiler sequence)
+    if (fn == 11) {
+        float a, b;
+        longer_pair(f2u(x), &a, &b);
+        return sqrt_(a) > sqrt_(b) ? 1.0f : 0.0f;  // glm length comparison as written
+    }
+    if (fn == 12) return u2f(f2u(x) / udiv_pair_d(f2u(x)));
     return math_fn(fn, x);
 }
 
@@ -1283,7 +1324,8 @@ __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long lo
         const uint32_t b = (uint32_t)(lo + i);
         const float x = u2f(b);
         const float a = math_fn(fn, x), e = math_fn_exact(fn, x);
-        if (!(f2u(a) == f2u(e) || (a != a && e != e))) {
+        // fn 10: a zero quotient's sign is not observed by the callers
+        if (!(f2u(a) == f2u(e) || (a != a && e != e) || (fn == 10 && a == 0.0f && e == 0.0f))) {
             ++local;
             atomicMin(first, b);
         }
@@ -1939,7 +1981,7 @@ int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms) {
 }
 
 int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
-    if (!in || !out || n < 0 || fn < 0 || fn > 9) return IPT_E_INVALID;
+    if (!in || !out || n < 0 || fn < 0 || fn > 12) return IPT_E_INVALID;
     const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
@@ -1951,7 +1993,7 @@ int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
 }
 
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n) {
-    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 9) return IPT_E_INVALID;
+    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 12) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     float *din = nullptr, *dout = nullptr;
     HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * 4));
@@ -2018,7 +2060,7 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
                        uint32_t* first_bad) {
-    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 9 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 12 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
         return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     unsigned long long* d_bad = nullptr;

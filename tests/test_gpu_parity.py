@@ -108,13 +108,18 @@ def test_cli_render_matches_oracle(gpu_ctx, oracle, tmp_path):
     assert (tmp_path / "r.png").read_bytes()[:4] == b"\x89PNG"
 
 
-@pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs"])
+@pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs", "div_inrange_pairs", "longer_pairs",
+                                "udiv_exact_pairs"])
 def test_fast_math_exhaustive(gpu_ctx, fn):
     """The device fast paths equal their exact references on all 2^32 inputs:
     (float)acos((double)x) (Ziv test + exact fallback) vs the fdlibm
     restatement (== glibc on every float, test_math_exhaustive.py); sqrtf and
     a/b (range-guarded correction cores, ipt_math.h) vs the compiler's IEEE
-    sequences (division over 2^32 in-range / zero-numerator pairs)."""
+    sequences (division over 2^32 in-range / zero-numerator pairs); the
+    range-free division of the box planes (div_inrange_) over the same pairs;
+    the squares-first length comparison (longer_sq) against sqrtf(x) >
+    sqrtf(y) over 2^32 near-tie and unrelated pairs; the 32-bit work-unit
+    decomposition (udiv_exact) against integer division over 2^32 pairs."""
     bad, first = gpu_ctx.math_selfcheck(capi.MATH_FNS[fn])
     assert bad == 0, (fn, bad, hex(first))
 
