@@ -716,8 +716,16 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
         }
         if (IPT_PROF && wave == 0) { IPT_PHASE(11); }  // workgroup steps (one wave counts)
         IPT_STAMP_AT(4);  // task posting, iteration prologue, Philox
-        // barrier A; also the block-wide exit test (every wave runs every barrier)
-        if (!__syncthreads_or(active ? 1 : 0)) break;
+        // barrier A; also the block-wide exit test (every wave runs every barrier):
+        // a wave with an active lane raises this step's flag (xcnt[par*2+1],
+        // cleared for the other parity after the barrier) — one s_barrier,
+        // where __syncthreads_or costs three
+        {
+            const uint64_t am = __ballot(active);
+            if (am && lane == __ffsll((long long)am) - 1) xcnt[par * 2 + 1] = 1;
+        }
+        __syncthreads();
+        if (xcnt[par * 2 + 1] == 0) break;
         IPT_STAMP_AT(5);  // barrier A
         if (tid == 0) {
             xcnt[(1 - par) * 2 + 0] = 0;
