@@ -242,7 +242,10 @@ inline bool bvh_build_lights(int n, const float (*P)[3], const float (*x)[3], co
         }
     }
     std::vector<int> perm;
-    bvh_build_boxes(box, 2, false, 1, nodes, perm, nodes_per_order);
+#ifndef IPT_LBVH_LEAF
+#define IPT_LBVH_LEAF 2
+#endif
+    bvh_build_boxes(box, IPT_LBVH_LEAF, false, 1, nodes, perm, nodes_per_order);
     return true;
 }
 

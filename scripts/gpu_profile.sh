@@ -20,7 +20,7 @@ python - <<PY
 import json
 for f in ("bench_$T", "bench_${T}_c3", "bench_${T}_c5"):
     d = json.load(open(f"gpurun_out/{f}.json")); r = d["roofline"] or {}; c = d.get("cpu_baseline") or {}
-    print(f, round(d["value"], 3), d["unit"], "ms/step", round(d["ms_per_step"], 1), "frac", r.get("frac"), "traffic", r.get("traffic"), "cpu", c.get("value"))
+    print(f, round(d["value"], 3), d["unit"], "ms/step", round(d["ms_per_step"], 1), "hbm_frac", r.get("frac"), "valu_frac", (r.get("valu") or {}).get("frac"), "traffic", r.get("traffic"), "cpu", c.get("value"))
 PY
 # the summaries written into profiles/ on the box travel back via gpurun_out/
 mkdir -p gpurun_out/profiles && cp profiles/${T}_* profiles/pmc_latest.json gpurun_out/profiles/
