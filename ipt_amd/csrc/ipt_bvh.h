@@ -205,6 +205,115 @@ inline void bvh_build_spheres(const float* cr, int n, const float cam[3], float 
     }
 }
 
+// Uniform grid over the sphere list (IPT_GEOM_SPHERES_IN_BOX, many small
+// spheres — BASELINE configs[2]): a ray walks the cells it crosses in order
+// (3D DDA) and stops once the next cell starts beyond the best hit, so a walk
+// costs the cells along the (short) ray instead of a root-to-leaf descent per
+// candidate. Exactness, with the BVH's padded sphere boxes and margin:
+// * every padded box (ipt_bvh.h header) is registered, inflated by m, in every
+//   cell it overlaps (ranges computed in double, rounded outward);
+// * the DDA's float rounding (approximate reciprocals, cell-boundary t's) can
+//   only make it visit a cell adjacent to the exact ray's where the ray passes
+//   within ~1e-6 |t| of a cell edge — far inside m = 1e-4 (1 + max |coord|),
+//   so every padded box the exact ray meets is registered in a visited cell;
+// * it stops after a cell whose exit t exceeds (best*1.0001 + 1e-5 + tmargin
+//   + m) * (1 + 1e-5) + 1e-5: a sphere registered only in later cells has its
+//   padded box entry beyond that, and (tmargin: tangency t-error) cannot
+//   produce a computed t below or equal to best;
+// * ties: equal t is broken by the lowest original index, as in the BVH
+//   (spheres registered in several cells are tested again, harmlessly).
+struct SphereGrid {
+    float g0[3], h[3], inv_h[3];
+    int n[3];
+    float m, tmargin;
+    std::vector<int> start;         // [cells + 1]
+    std::vector<BvhSphere> items;   // per-cell sphere records
+};
+
+#ifndef IPT_GRID_CELLS_PER_SPHERE
+#define IPT_GRID_CELLS_PER_SPHERE 3.0
+#endif
+inline bool grid_build_spheres(const float* cr, int n, const float cam[3], float B, SphereGrid& g) {
+    if (n <= 0) return false;
+    std::vector<double> lo(3 * (size_t)n), hi(3 * (size_t)n);
+    double glo[3] = {INFINITY, INFINITY, INFINITY}, ghi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double tm = 0.0, maxabs = std::max(std::fabs((double)cam[0]), std::max(std::fabs((double)cam[1]), std::fabs((double)cam[2])));
+    for (int i = 0; i < n; ++i) {
+        const float r = cr[4 * i + 3];
+        float blo[3], bhi[3];
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = cr[4 * i + a] - r;
+            bhi[a] = cr[4 * i + a] + r;
+        }
+        const double D = origin_bound(cam, B, blo, bhi);
+        const double cn = std::fabs((double)cr[4 * i]) + std::fabs((double)cr[4 * i + 1]) +
+                          std::fabs((double)cr[4 * i + 2]);
+        const double pad = (std::sqrt((double)r * r + 4e-6 * D * D) - r) + 1e-4 * (cn + r + 1.0);
+        if (!std::isfinite(pad) || !std::isfinite(cn) || !(r >= 0.0f)) return false;
+        tm = std::max(tm, 1e-3 * D);
+        for (int a = 0; a < 3; ++a) {
+            lo[3 * (size_t)i + a] = (double)blo[a] - pad;
+            hi[3 * (size_t)i + a] = (double)bhi[a] + pad;
+            glo[a] = std::min(glo[a], lo[3 * (size_t)i + a]);
+            ghi[a] = std::max(ghi[a], hi[3 * (size_t)i + a]);
+            maxabs = std::max(maxabs, std::max(std::fabs(glo[a]), std::fabs(ghi[a])));
+        }
+    }
+    const double m = 1e-4 * (1.0 + maxabs);
+    double ext[3], vol = 1.0;
+    for (int a = 0; a < 3; ++a) {
+        glo[a] -= 2.0 * m;
+        ghi[a] += 2.0 * m;
+        ext[a] = ghi[a] - glo[a];
+        vol *= ext[a];
+    }
+    const double hc = std::cbrt(vol / (IPT_GRID_CELLS_PER_SPHERE * n));
+    size_t cells = 1;
+    for (int a = 0; a < 3; ++a) {
+        g.n[a] = (int)std::min(256.0, std::max(1.0, std::round(ext[a] / hc)));
+        g.h[a] = (float)(ext[a] / g.n[a]);
+        g.g0[a] = (float)glo[a];
+        g.inv_h[a] = 1.0f / g.h[a];
+        cells *= (size_t)g.n[a];
+    }
+    g.m = (float)m;
+    g.tmargin = (float)(tm * (1.0 + 1e-6)) + 1e-7f;
+    // cell range of an inflated box, rounded outward, in double
+    auto range = [&](int a, double l, double h2, int* i0, int* i1) {
+        const double f0 = (l - m - (double)g.g0[a]) / (double)g.h[a], f1 = (h2 + m - (double)g.g0[a]) / (double)g.h[a];
+        *i0 = (int)std::max(0.0, std::floor(f0 - 1e-9));
+        *i1 = (int)std::min((double)g.n[a] - 1, std::floor(f1 + 1e-9));
+    };
+    g.start.assign(cells + 1, 0);
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<int> fill;
+        if (pass == 1) {
+            for (size_t c = 0; c < cells; ++c) g.start[c + 1] += g.start[c];
+            g.items.resize(g.start[cells]);
+            fill.assign(g.start.begin(), g.start.end() - 1);
+        }
+        for (int i = 0; i < n; ++i) {
+            int r0[3], r1[3];
+            for (int a = 0; a < 3; ++a) range(a, lo[3 * (size_t)i + a], hi[3 * (size_t)i + a], &r0[a], &r1[a]);
+            for (int z = r0[2]; z <= r1[2]; ++z)
+                for (int y = r0[1]; y <= r1[1]; ++y)
+                    for (int x = r0[0]; x <= r1[0]; ++x) {
+                        const size_t c = (size_t)x + (size_t)g.n[0] * ((size_t)y + (size_t)g.n[1] * z);
+                        if (pass == 0) {
+                            ++g.start[c + 1];
+                        } else {
+                            BvhSphere sp{};
+                            for (int a = 0; a < 3; ++a) sp.c[a] = cr[4 * i + a];
+                            sp.r = cr[4 * i + 3];
+                            sp.index = i;
+                            g.items[fill[c]++] = sp;
+                        }
+                    }
+        }
+    }
+    return true;
+}
+
 // Light BVH over index ranges (one order, leaves of <= 2 lights, items in
 // index order). P, x, y: corner and axes; inv: inverse(mat3(x, y, cross)) as
 // the trace uses it (9 floats). Returns false (no BVH) when a light is

@@ -56,6 +56,12 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_RESUME
 #define IPT_RESUME 1  // sphere-BVH walks bounded per step and resumed in later steps
 #endif
+#ifndef IPT_GRID_BUDGET
+#define IPT_GRID_BUDGET 8  // grid cells per lane per step of a resumable walk (measured: 4-32)
+#endif
+#ifndef IPT_SPHERE_GRID
+#define IPT_SPHERE_GRID 1  // uniform grid instead of the BVH for large sphere lists inside the box
+#endif
 #ifndef IPT_WALK_BUDGET
 #define IPT_WALK_BUDGET 48  // node visits per lane per step of a resumable walk
 #endif
@@ -132,7 +138,12 @@ struct KParams {
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int n_spheres;
     const float4* __restrict__ spheres;   // (c.xyz, r)
-    float bvh_tmargin;                    // sphere BVH: additive pruning margin (1e-3 D, ipt_bvh.h)
+    float bvh_tmargin;                    // sphere BVH / grid: additive pruning margin (1e-3 D, ipt_bvh.h)
+    int n_grid;                           // > 0: uniform sphere grid (ipt_bvh.h SphereGrid) instead of the BVH
+    float grid_g0[3], grid_h[3], grid_inv_h[3], grid_m;
+    int grid_n[3];
+    const int* __restrict__ grid_start;   // [cells + 1]
+    const BvhSphere* __restrict__ grid_items;
     const BvhNode* __restrict__ bvh_nodes;     // n_nodes > 0: sphere BVH (ipt_bvh.h)
     const BvhSphere* __restrict__ bvh_prims;
     int n_nodes;
@@ -289,6 +300,86 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
 #endif
 }
 
+// Uniform-grid walk (ipt_bvh.h SphereGrid; exactness argument there). The
+// resumable state is the current cell (x | y << 8 | z << 16, -1 when done) and
+// the t of the next cell boundary per axis.
+__device__ __forceinline__ void sphere_grid_init(const KParams& kp, vec3 o, vec3 d, int& cell, vec3& tmx) {
+    const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    const float dv[3] = {d.x, d.y, d.z}, ov[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
+    float tn = 0.0f, tf = inf_();
+    for (int a = 0; a < 3; ++a) {
+        const float g1 = kp.grid_g0[a] + (float)kp.grid_n[a] * kp.grid_h[a];
+        if (dv[a] == 0.0f) {
+            if (ov[a] < kp.grid_g0[a] || ov[a] > g1) tf = -1.0f;  // parallel and outside
+            continue;
+        }
+        const float t0 = (kp.grid_g0[a] - ov[a]) * iv[a], t1 = (g1 - ov[a]) * iv[a];
+        tn = fmaxf(tn, fminf(t0, t1));
+        tf = fminf(tf, fmaxf(t0, t1));
+    }
+    if (!(tn <= tf * 1.0001f + 1e-5f)) {
+        cell = -1;
+        return;
+    }
+    int ia[3];
+    float tm[3];
+    for (int a = 0; a < 3; ++a) {
+        const float pa = ov[a] + dv[a] * tn;
+        int c = (int)floorf((pa - kp.grid_g0[a]) * kp.grid_inv_h[a]);
+        c = c < 0 ? 0 : (c >= kp.grid_n[a] ? kp.grid_n[a] - 1 : c);
+        ia[a] = c;
+        tm[a] = dv[a] > 0.0f   ? ((kp.grid_g0[a] + (float)(c + 1) * kp.grid_h[a]) - ov[a]) * iv[a]
+                : dv[a] < 0.0f ? ((kp.grid_g0[a] + (float)c * kp.grid_h[a]) - ov[a]) * iv[a]
+                               : inf_();
+    }
+    cell = ia[0] | ia[1] << 8 | ia[2] << 16;
+    tmx = v3(tm[0], tm[1], tm[2]);
+}
+template <bool COUNT>
+__device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3 d, int& cell, vec3& tmx, float& best,
+                                                 int& bidx, int budget, uint32_t& c_nodes, uint32_t& c_tests) {
+    const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    while (cell >= 0 && budget-- > 0) {
+        const int ix = cell & 0xff, iy = (cell >> 8) & 0xff, iz = cell >> 16;
+        const int lin = ix + kp.grid_n[0] * (iy + kp.grid_n[1] * iz);
+        const int s0 = kp.grid_start[lin], s1 = kp.grid_start[lin + 1];
+        if (COUNT) {
+            ++c_nodes;
+            c_tests += (uint32_t)(s1 - s0);
+        }
+        for (int k2 = s0; k2 < s1; ++k2) {
+            const BvhSphere sp = kp.grid_items[k2];
+            const float t = sphere_t(sp.r, o - v3(sp.c[0], sp.c[1], sp.c[2]), d);
+            if (isfinite_(t) && gt_1em6(fabs_(t)) && (t < best || (t == best && bidx >= 0 && sp.index < bidx))) {
+                best = t;
+                bidx = sp.index;
+            }
+        }
+        const float texit = fminf(fminf(tmx.x, tmx.y), tmx.z);
+        if (texit > (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f) {
+            cell = -1;
+            break;
+        }
+        // step across the nearest boundary (x, then y, then z on ties)
+        if (tmx.x <= tmx.y && tmx.x <= tmx.z) {
+            const int nx = d.x > 0.0f ? ix + 1 : ix - 1;
+            if (nx < 0 || nx >= kp.grid_n[0]) { cell = -1; break; }
+            cell = (cell & ~0xff) | nx;
+            tmx.x = ((kp.grid_g0[0] + (float)(d.x > 0.0f ? nx + 1 : nx) * kp.grid_h[0]) - o.x) * inv.x;
+        } else if (tmx.y <= tmx.z) {
+            const int ny = d.y > 0.0f ? iy + 1 : iy - 1;
+            if (ny < 0 || ny >= kp.grid_n[1]) { cell = -1; break; }
+            cell = (cell & ~0xff00) | ny << 8;
+            tmx.y = ((kp.grid_g0[1] + (float)(d.y > 0.0f ? ny + 1 : ny) * kp.grid_h[1]) - o.y) * inv.y;
+        } else {
+            const int nz = d.z > 0.0f ? iz + 1 : iz - 1;
+            if (nz < 0 || nz >= kp.grid_n[2]) { cell = -1; break; }
+            cell = (cell & 0xffff) | nz << 16;
+            tmx.z = ((kp.grid_g0[2] + (float)(d.z > 0.0f ? nz + 1 : nz) * kp.grid_h[2]) - o.z) * inv.z;
+        }
+    }
+}
+
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
 // r=0.5 sphere, 6+i extra sphere i (original index), -1 miss.
 template <bool COUNT, int GEOM>
@@ -348,7 +439,12 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
     if (GEOM == IPT_GEOM_SPHERES_IN_BOX)
         best = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(o, d, &p) : trace_box_planes_only<false>(o, d, &p);
     int bidx = -1;
-    if (kp.n_nodes > 0) {
+    if (kp.n_grid > 0) {
+        int cell;
+        vec3 tmx;
+        sphere_grid_init(kp, o, d, cell, tmx);
+        sphere_grid_walk<COUNT>(kp, o, d, cell, tmx, best, bidx, 0x7fffffff, c_nodes, c_tests);
+    } else if (kp.n_nodes > 0) {
         int i = 0;
         sphere_bvh_walk<COUNT>(kp, o, d, i, best, bidx, 0x7fffffff, c_nodes, c_tests);
     } else {
@@ -536,6 +632,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
     int xrdepth = 0, xi = 0, xbidx = -1, xp = -1;
     bool xis_iter = false, xhas_li = false;
     float xmult = 0.0f, xli_pow = 0.0f, xbest = 0.0f;
+    vec3 xtm = v3(0, 0, 0);  // grid walk: t of the next cell boundaries
     float tres = 0.0f;
     int ti = 0, tdepth = 0, tkind = 0;  // kind: 0..4 wall plane, 5 box sphere, 6+i extra sphere i
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
@@ -1008,7 +1105,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 mult = div_(sdf_val, mix);
             }
             // child ray_power (main.cpp:100-143): the geometry trace, then resolve
-            if (kRes && rdepth < kp.depth_max && kp.n_nodes > 0) {
+            if (kRes && rdepth < kp.depth_max && (kp.n_nodes > 0 || kp.n_grid > 0)) {
                 // resumable walk: keep the ray and the light results, planes now
                 xro = ro;
                 xrd = rd;
@@ -1025,6 +1122,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 if (GEOM == IPT_GEOM_SPHERES_IN_BOX)
                     xbest = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(ro, rd, &xp)
                                                            : trace_box_planes_only<false>(ro, rd, &xp);
+                if (kp.n_grid > 0) sphere_grid_init(kp, ro, rd, xi, xtm);
                 tracing = true;
             } else {
                 int prim = -1;
@@ -1044,8 +1142,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
         }
         if (kRes && tracing) {
             IPT_PHASE(9);
-            sphere_bvh_walk<COUNT>(kp, xro, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
-            if (xi >= kp.n_nodes) {
+            bool done;
+            if (kp.n_grid > 0) {
+                sphere_grid_walk<COUNT>(kp, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET, c_nodes, c_tests);
+                done = xi < 0;
+            } else {
+                sphere_bvh_walk<COUNT>(kp, xro, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
+                done = xi >= kp.n_nodes;
+            }
+            if (done) {
                 tracing = false;
                 resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : xp, xro, xrd, xrdepth, xis_iter, xmult, xhas_li, xli_pos,
                         xli_pow);
@@ -1366,6 +1471,10 @@ struct ipt_ctx {
     BvhSphere* d_bvh_prims = nullptr;
     int n_nodes = 0;
     float bvh_tmargin = 0.0f;  // sphere BVH pruning margin (ipt_bvh.h)
+    SphereGrid grid;           // geometry of the uniform sphere grid (host copy)
+    int n_grid = 0;
+    int* d_grid_start = nullptr;
+    BvhSphere* d_grid_items = nullptr;
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
@@ -1619,6 +1728,16 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.spheres = ctx->d_spheres;
         kp.bvh_nodes = ctx->d_bvh_nodes;
         kp.bvh_tmargin = ctx->bvh_tmargin;
+        kp.n_grid = ctx->n_grid;
+        for (int a = 0; a < 3; ++a) {
+            kp.grid_g0[a] = ctx->grid.g0[a];
+            kp.grid_h[a] = ctx->grid.h[a];
+            kp.grid_inv_h[a] = ctx->grid.inv_h[a];
+            kp.grid_n[a] = ctx->grid.n[a];
+        }
+        kp.grid_m = ctx->grid.m;
+        kp.grid_start = ctx->d_grid_start;
+        kp.grid_items = ctx->d_grid_items;
         kp.bvh_prims = ctx->d_bvh_prims;
         kp.n_nodes = ctx->n_nodes;
         kp.light_nodes = ctx->d_light_nodes;
@@ -1737,7 +1856,8 @@ void ipt_destroy(ipt_ctx* ctx) {
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
-                    ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b};
+                    ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
+                    ctx->d_grid_start, ctx->d_grid_items};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& e : ctx->ev)
@@ -1802,7 +1922,13 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     std::vector<BvhSphere> bprims;
     int per_order = 0;
     float tmargin = 0.0f;
-    if ((s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX || s->geometry_kind == IPT_GEOM_SPHERES) && s->n_spheres > 16)
+    // many spheres inside the box: a uniform grid; otherwise (and if the grid
+    // cannot be built) the BVH
+    SphereGrid grid;
+    bool use_grid = IPT_SPHERE_GRID && s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX && s->n_spheres > 256 &&
+                    grid_build_spheres(reinterpret_cast<const float*>(sph.data()), s->n_spheres, cam, B, grid);
+    if (!use_grid && (s->geometry_kind == IPT_GEOM_SPHERES_IN_BOX || s->geometry_kind == IPT_GEOM_SPHERES) &&
+        s->n_spheres > 16)
         bvh_build_spheres(reinterpret_cast<const float*>(sph.data()), s->n_spheres, cam, B, bnodes, bprims,
                           &per_order, &tmargin);
     // light BVH: only for the global-memory light mode (n_lights > kLdsLights)
@@ -1833,7 +1959,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     for (int i = 0; i <= nl; ++i)
         if (!(cdf[i] == cdf[i]) || (i > 0 && !(cdf[i - 1] <= cdf[i]))) cdf_mono = false;
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes,
-                   ctx->d_bvh_prims, ctx->d_light_nodes};
+                   ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_lights = nullptr;
@@ -1844,6 +1970,22 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->n_nodes = 0;
     ctx->d_light_nodes = nullptr;
     ctx->n_light_nodes = 0;
+    ctx->d_grid_start = nullptr;
+    ctx->d_grid_items = nullptr;
+    ctx->n_grid = 0;
+    if (use_grid) {
+        HIPCHECK(ctx, hipMalloc(&ctx->d_grid_start, sizeof(int) * grid.start.size()));
+        HIPCHECK(ctx, hipMalloc(&ctx->d_grid_items, sizeof(BvhSphere) * std::max<size_t>(1, grid.items.size())));
+        HIPCHECK(ctx, hipMemcpy(ctx->d_grid_start, grid.start.data(), sizeof(int) * grid.start.size(), hipMemcpyHostToDevice));
+        if (!grid.items.empty())
+            HIPCHECK(ctx, hipMemcpy(ctx->d_grid_items, grid.items.data(), sizeof(BvhSphere) * grid.items.size(),
+                                    hipMemcpyHostToDevice));
+        ctx->n_grid = (int)(grid.start.size() - 1);
+        ctx->bvh_tmargin = grid.tmargin;
+        grid.start.clear();
+        grid.items.clear();
+        ctx->grid = grid;
+    }
     if (!lnodes.empty()) {
         HIPCHECK(ctx, hipMalloc(&ctx->d_light_nodes, sizeof(BvhNode) * lnodes.size()));
         HIPCHECK(ctx, hipMemcpy(ctx->d_light_nodes, lnodes.data(), sizeof(BvhNode) * lnodes.size(),

@@ -285,3 +285,37 @@ def test_light_bvh_in_lds_bit_exact(oracle, monkeypatch, desc_fn):
         assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
     finally:
         ctx.close()
+
+
+def _lattice_scene(k, r, cam_pos, cam_dir):
+    sp = []
+    for i in range(k):
+        for j in range(k):
+            for m in range(k):
+                c = [float(np.float32(-0.8 + 1.6 * (q + 0.5) / k)) for q in (i, j, m)]
+                sp.append((c, float(np.float32(r))))
+    d = scenes.make_scene_spheres(1, seed=1)
+    d["spheres"] = sp
+    d["camera"] = scenes.simple_camera(cam_pos, cam_dir)
+    return d
+
+
+@pytest.mark.parametrize("k,r,cam_pos,cam_dir", [
+    (10, 0.03, (0.0, -3.0, 0.0), (0.0, 1.0, 0.0)),      # axis-aligned camera, rays along lattice rows
+    (8, 0.09, (0.05, 0.0, 0.05), (0.3, 1.0, 0.2)),      # overlapping spheres, camera inside the grid
+    (12, 0.02, (-0.95, -0.95, -0.95), (1.0, 1.0, 1.0)),  # diagonal through cell corners
+])
+def test_sphere_grid_adversarial_bit_exact(gpu_ctx, oracle, k, r, cam_pos, cam_dir):
+    """The uniform sphere grid (> 256 spheres inside the box) on lattices whose
+    rows line up with the camera, overlapping spheres around an inside camera,
+    and a diagonal view through cell corners: the DDA walk with its outward
+    registration and stopping margin must reproduce the oracle's linear scan
+    (FractalSpheres.cpp:75-84) bit for bit."""
+    desc = _lattice_scene(k, r, cam_pos, cam_dir)
+    p = capi.make_params(16, 12, 1, n_rays=8, depth_max=5)
+    gpu_ctx.upload_scene(desc)
+    gpu_ctx.reset_counters()
+    gv, gc = gpu_ctx.render_values(p)
+    ov, oc = ob.render_values(desc, p, 0)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
