@@ -62,6 +62,12 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_SPHERE_GRID
 #define IPT_SPHERE_GRID 1  // uniform grid instead of the BVH for large sphere lists inside the box
 #endif
+#ifndef IPT_RESUME_LIGHTS
+#define IPT_RESUME_LIGHTS 1  // light-BVH walks bounded per step and resumed (many-light scenes)
+#endif
+#ifndef IPT_LWALK_BUDGET
+#define IPT_LWALK_BUDGET 16  // light-BVH nodes per lane per step of a resumable walk
+#endif
 #ifndef IPT_WALK_BUDGET
 #define IPT_WALK_BUDGET 48  // node visits per lane per step of a resumable walk
 #endif
@@ -536,11 +542,18 @@ struct LightSet {
 // neither the sphere-list code nor its pointers (SGPR pressure).
 // Sphere-list instances carry the resumable walk's state (IPT_RESUME): they
 // are given 3 waves per SIMD of registers (their LDS allows 3 workgroups).
-__host__ __device__ constexpr int waves_per_simd(int geom) {
-    return (IPT_RESUME && (geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES)) ? 3 : IPT_WAVES_PER_SIMD;
+__host__ __device__ constexpr bool resumable_geom(int geom) {
+    return IPT_RESUME && (geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES);
+}
+// many-light instances without a sphere list resume their light-BVH walk the same way
+__host__ __device__ constexpr bool resumable_lights(int lmode, int geom) {
+    return IPT_RESUME_LIGHTS && lmode == 3 /* kLightsGlobal */ && !resumable_geom(geom);
+}
+__host__ __device__ constexpr int waves_per_simd(int geom, int lmode) {
+    return (resumable_geom(geom) || resumable_lights(lmode, geom)) ? 3 : IPT_WAVES_PER_SIMD;
 }
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
-__global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(const KParams kp) {
+__global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
     constexpr int kFrameSlots = frame_slots(GEOM);
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
@@ -626,8 +639,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
     // done within IPT_WALK_BUDGET node visits keeps its ray and light results
     // and resumes the walk in the next steps (doing nothing else meanwhile), so
     // a step costs the budget, not the longest walk of the workgroup.
-    constexpr bool kRes = IPT_RESUME && (GEOM == IPT_GEOM_SPHERES_IN_BOX || GEOM == IPT_GEOM_SPHERES);
-    bool tracing = false;
+    constexpr bool kRes = resumable_geom(GEOM);
+    constexpr bool kResL = resumable_lights(LMODE, GEOM);
+    bool tracing = false;  // a resumable walk (sphere list or light BVH) is in progress
+    float xlmix = 0.0f;    // light walk: the running UnionDdf light sum
     vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
     int xrdepth = 0, xi = 0, xbidx = -1, xp = -1;
     bool xis_iter = false, xhas_li = false;
@@ -687,7 +702,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
         IPT_STAMP_AT(1);  // refill
         if (active) { IPT_PHASE(0); }
         // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
-        if (active && has_path && !fresh && !(kRes && tracing)) {
+        if (active && has_path && !fresh && !((kRes || kResL) && tracing)) {
             for (;;) {
                 const int n = kp.n_rays >> tdepth;
                 if (ti < n) break;
@@ -723,7 +738,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
         // workgroup (RotateDdf frames of sphere nodes, CosineDdf local samples) so
         // that they run on ceil(N/64) dense wave-passes instead of on every wave.
         const int par = step & 1;
-        bool want_frame = need_frame && has_path && !fresh && !(kRes && tracing);
+        bool want_frame = need_frame && has_path && !fresh && !((kRes || kResL) && tracing);
         int slot_f = 0;
         {
             const uint64_t m = __ballot(want_frame);
@@ -753,7 +768,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
             xfr[3 * kFrameSlots + slot_f] = __int_as_float(tid);
         }
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
-        const bool iter_lane = active && has_path && !fresh && !stalled && !(kRes && tracing);
+        const bool iter_lane = active && has_path && !fresh && !stalled && !((kRes || kResL) && tracing);
         int pick = -1;
         float u1 = 0.0f, u2 = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
         if (iter_lane) {
@@ -1018,6 +1033,95 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                 has_path = false;
             }
         };
+        if constexpr (kResL) {
+            // many lights: the light-BVH walk (same order and arithmetic as the
+            // full walk below) is bounded per step and resumed; then the mixture
+            // value, the geometry trace and resolve, as below
+            if (have_ray) {
+                IPT_PHASE(8);
+                if (COUNT) c_ltr += (uint32_t)nl * ((is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u));
+                xro = ro;
+                xrd = rd;
+                xrdepth = rdepth;
+                xis_iter = is_iter;
+                xlmix = 0.0f;
+                xhas_li = false;
+                xli_pos = v3(0, 0, 0);
+                xli_pow = 0.0f;
+                xi = 0;
+                tracing = true;
+            }
+            if (tracing) {
+                if (kp.n_light_nodes > 0) {
+                    const vec3 inv = v3(safe_rcp(xrd.x), safe_rcp(xrd.y), safe_rcp(xrd.z));
+                    int budget = IPT_LWALK_BUDGET;
+                    while (xi < kp.n_light_nodes && budget > 0) {
+                        int leaf = -1;
+                        while (xi < kp.n_light_nodes && budget > 0) {
+                            --budget;
+                            const BvhNode nd = kp.light_nodes[xi];
+                            if (COUNT) ++c_lnode;
+                            const bool enter = bvh_box_entry(nd, xro, inv) != inf_();
+                            if (enter && nd.leaf >= 0) {
+                                leaf = nd.leaf;
+                                xi = nd.skip;
+                                break;
+                            }
+                            xi = enter ? xi + 1 : nd.skip;
+                        }
+                        if (leaf >= 0) {
+                            const int first = leaf & 0xffffff, cnt = leaf >> 24;
+                            for (int l = first; l < first + cnt; ++l) {
+                                const LightDev& L = LS.light(l);
+                                vec3 hp, hn;
+                                const bool h = light_trace<false>(L, xro, xrd, &hp, &hn);
+                                if (COUNT) ++c_ltest;
+                                if (xis_iter) xlmix += LS.weight(l) * light_pdf(L, xro, h, hp, hn);
+                                if (h && (!xhas_li || longer(xli_pos - xro, hp - xro))) {
+                                    xhas_li = true;
+                                    xli_pos = hp;
+                                    xli_pow = L.spow;
+                                }
+                            }
+                        }
+                    }
+                } else {
+                    for (int l = 0; l < nl; ++l) {
+                        const LightDev& L = LS.light(l);
+                        vec3 hp, hn;
+                        const bool h = light_trace<false>(L, xro, xrd, &hp, &hn);
+                        if (COUNT) ++c_ltest;
+                        if (xis_iter) xlmix += LS.weight(l) * light_pdf(L, xro, h, hp, hn);
+                        if (h && (!xhas_li || longer(xli_pos - xro, hp - xro))) {
+                            xhas_li = true;
+                            xli_pos = hp;
+                            xli_pow = L.spow;
+                        }
+                    }
+                    xi = kp.n_light_nodes;
+                }
+                if (xi >= kp.n_light_nodes) {
+                    tracing = false;
+                    float mult = 0.0f;
+                    if (xis_iter) {
+                        const float* fc = lfr + (tkind < 5 ? kBlock + tkind : tid);
+                        Frame fz;
+                        fz.iz = v3(fc[9 * kFrameStride], fc[10 * kFrameStride], fc[11 * kFrameStride]);
+                        const float sdf_val = frame_cosine_value(fz, xrd);
+                        const float mix = xlmix + w_sdf * sdf_val;
+                        mult = div_(sdf_val, mix);
+                    }
+                    int prim = -1;
+                    float t = inf_();
+                    if (xrdepth < kp.depth_max) {
+                        IPT_PHASE(9);
+                        t = trace_geometry<COUNT, GEOM>(kp, xro, xrd, &prim, c_nodes, c_tests);
+                    }
+                    resolve(xrdepth < kp.depth_max, t, prim, xro, xrd, xrdepth, xis_iter, mult, xhas_li, xli_pos,
+                            xli_pow);
+                }
+            }
+        } else {
         if (have_ray) {
             IPT_PHASE(8);
             // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
@@ -1156,6 +1260,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM)) void path_kernel(cons
                         xli_pow);
             }
         }
+        }  // !kResL
     }
 
     if (IPT_STAMP && lane == 0)
