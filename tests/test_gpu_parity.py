@@ -270,12 +270,14 @@ def test_spheres_in_box_bit_exact(gpu_ctx, oracle, n):
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
 
 
+@pytest.mark.parametrize("lds", ["0", "1"])
 @pytest.mark.parametrize("desc_fn", [lambda: scenes.make_scene_box_lights(16),
                                      lambda: scenes.make_scene_random_lights(300, seed=7)])
-def test_light_bvh_in_lds_bit_exact(oracle, monkeypatch, desc_fn):
-    """The optional LDS-staged light BVH (IPT_LNODES_LDS=1, read at ipt_create)
-    walks the same nodes as the global-memory copy: bit-exact vs the oracle."""
-    monkeypatch.setenv("IPT_LNODES_LDS", "1")
+def test_light_bvh_in_lds_bit_exact(oracle, monkeypatch, desc_fn, lds):
+    """The light BVH staged in LDS (default) and kept in global memory
+    (IPT_LNODES_LDS=0, read at ipt_create) walk the same nodes: bit-exact vs
+    the oracle."""
+    monkeypatch.setenv("IPT_LNODES_LDS", lds)
     ctx = capi.Context(0)
     try:
         desc = desc_fn()
