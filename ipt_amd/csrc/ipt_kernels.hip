@@ -549,8 +549,11 @@ __host__ __device__ constexpr bool resumable_geom(int geom) {
 __host__ __device__ constexpr bool resumable_lights(int lmode, int geom) {
     return IPT_RESUME_LIGHTS && lmode == 3 /* kLightsGlobal */ && !resumable_geom(geom);
 }
+#ifndef IPT_RES_WAVES
+#define IPT_RES_WAVES 3
+#endif
 __host__ __device__ constexpr int waves_per_simd(int geom, int lmode) {
-    return (resumable_geom(geom) || resumable_lights(lmode, geom)) ? 3 : IPT_WAVES_PER_SIMD;
+    return (resumable_geom(geom) || resumable_lights(lmode, geom)) ? IPT_RES_WAVES : IPT_WAVES_PER_SIMD;
 }
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
