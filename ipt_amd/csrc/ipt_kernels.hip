@@ -475,22 +475,14 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
 constexpr int kLdsLights = 16;
 constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
 constexpr int kLdsCand = 512;
-// sphere-frame builds per workgroup step (overflow lanes retry next step):
-// the box scene makes ~25 per step, the sphere-list scene (nearly every hit a
-// sphere) well over 64
-__host__ __device__ constexpr int frame_slots(int geom) {
-    return geom == IPT_GEOM_SPHERES_IN_BOX || geom == IPT_GEOM_SPHERES || geom == IPT_GEOM_SMALLPT ? kBlock : kBlock / 4;
-}
-// LDS after the DFS stack: wall frames, [LMODE 2: lights, weights, cdf],
-// task counters, frame tasks, cosine tasks, [sharded: candidate rows] (last,
-// so unsharded launches do not allocate it).
-// CosineDdf samples come from exact tables (cos_table_kernel).
+// LDS after the DFS stack: frames, [LMODE 2: lights, weights, cdf],
+// [sharded: candidate rows], [LMODE 3: weights, cdf, light BVH].
 // Frames live in LDS, [12][kFrameStride]: column tid is the lane's current
 // sphere-node frame, columns kBlock..kBlock+4 the five wall frames.
+// CosineDdf samples come from exact tables (cos_table_kernel).
 constexpr int kFrameStride = kBlock + 8;
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
-    return 12 * (size_t)kFrameStride + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0) +
-           4 + 4 * (size_t)frame_slots(geom);
+    return 12 * (size_t)kFrameStride + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0);
 }
 // kLightsGlobal: mixture weights + CDF (and, when small, the light BVH) are
 // staged in LDS after the fixed layout: their global copies would be evicted
@@ -557,23 +549,20 @@ __host__ __device__ constexpr int waves_per_simd(int geom, int lmode) {
 }
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
-    constexpr int kFrameSlots = frame_slots(GEOM);
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
     float* lfr = lds + MAXSUSP * kStackFields * kBlock;       // [12][kFrameStride] lane + wall frames
     LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride);
     float* weights_lds = reinterpret_cast<float*>(lights_lds) + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
-    int* xcnt = reinterpret_cast<int*>(reinterpret_cast<float*>(lights_lds) +
-                                       (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
-    float* xfr = reinterpret_cast<float*>(xcnt + 4);          // [4][kFrameSlots] frame tasks: normal, lane
-    int* cand_lds = reinterpret_cast<int*>(xfr + 4 * kFrameSlots);  // [kLdsCand] when kp.cand_lds
+    int* cand_lds = reinterpret_cast<int*>(reinterpret_cast<float*>(lights_lds) +
+                                           (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
+                                           // [kLdsCand] when kp.cand_lds
     // kLightsGlobal: [weights | cdf | light BVH nodes] after the candidate rows
     float* gl_lds = reinterpret_cast<float*>(cand_lds) + (kp.cand_lds ? kLdsCand : 0);
     BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + ((2 * (kp.n_lights + 1) + 3) & ~3));
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
-    if (tid < 4) xcnt[tid] = 0;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
     const bool cand_in_lds = kp.cand_lds != 0;
     if (tid < 60) lfr[(tid % 12) * kFrameStride + kBlock + tid / 12] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
@@ -632,7 +621,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     // never stored: walls load theirs from the LDS table, sphere nodes rebuild
     // theirs (make_frame) in the frame phase of the step after a push or pop.
     bool active = true, has_path = false, fresh = false, need_frame = false, need_b = false;
-    uint32_t step = 0;
     unsigned long long unit = 0;
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
@@ -736,28 +724,16 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }
 
         IPT_STAMP_AT(2);  // finalize + pop
-        IPT_STAMP_AT(3);  // (new path: after barrier B)
-        // ------------- phase 3: post the step's expensive, divergent tasks to the
-        // workgroup (RotateDdf frames of sphere nodes, CosineDdf local samples) so
-        // that they run on ceil(N/64) dense wave-passes instead of on every wave.
-        const int par = step & 1;
-        bool want_frame = need_frame && has_path && !fresh && !((kRes || kResL) && tracing);
-        int slot_f = 0;
-        {
-            const uint64_t m = __ballot(want_frame);
-            if (m) {
-                const int first = __ffsll((long long)m) - 1;
-                int base = 0;
-                if (lane == first) base = atomicAdd(&xcnt[par * 2 + 0], __popcll(m));
-                base = __shfl(base, first);
-                slot_f = base + __popcll(m & lanemask_lt);
-            }
-        }
-        const bool stalled = want_frame && slot_f >= kFrameSlots;  // retry next step
-        if (want_frame && !stalled) {
+        IPT_STAMP_AT(3);  // (new path: later in the step)
+        // ------------- phase 3: the current node's RotateDdf frame when it is a sphere node without one
+        // (after a push, or a pop past a sphere descendant): built by the lane
+        // itself into its LDS column. Waves share no LDS after the setup, so they
+        // run without barriers (a pooled workgroup frame pass with two barriers
+        // per step measured 5-13 % slower).
+        if (need_frame && has_path && !fresh && !((kRes || kResL) && tracing)) {
             vec3 nrm;
             if (GEOM == IPT_GEOM_SPHERE_IN_BOX || tkind == 5) {
-                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67 (done by the worker)
+                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67
             } else {
                 const float4 sp = kp.spheres[tkind - 6];
                 nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
@@ -765,13 +741,19 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // normalize(-v) is the same bits (negation is exact)
                 if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
             }
-            xfr[0 * kFrameSlots + slot_f] = nrm.x;
-            xfr[1 * kFrameSlots + slot_f] = nrm.y;
-            xfr[2 * kFrameSlots + slot_f] = nrm.z;
-            xfr[3 * kFrameSlots + slot_f] = __int_as_float(tid);
+            IPT_PHASE(5);
+            const Frame f = make_frame(normalize(nrm));
+            if (IPT_ABL == 1) keep_alive(make_frame(normalize(nrm * (1.0f + kp.abl_zero))));
+            float* c = lfr + tid;
+            c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
+            c[3 * kFrameStride] = f.m1.x; c[4 * kFrameStride] = f.m1.y; c[5 * kFrameStride] = f.m1.z;
+            c[6 * kFrameStride] = f.m2.x; c[7 * kFrameStride] = f.m2.y; c[8 * kFrameStride] = f.m2.z;
+            c[9 * kFrameStride] = f.iz.x; c[10 * kFrameStride] = f.iz.y; c[11 * kFrameStride] = f.iz.z;
+            need_frame = false;
+            fdepth = tdepth;
         }
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
-        const bool iter_lane = active && has_path && !fresh && !stalled && !((kRes || kResL) && tracing);
+        const bool iter_lane = active && has_path && !fresh && !((kRes || kResL) && tracing);
         int pick = -1;
         float u1 = 0.0f, u2 = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
         if (iter_lane) {
@@ -832,48 +814,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }
         if (IPT_PROF && wave == 0) { IPT_PHASE(11); }  // workgroup steps (one wave counts)
         IPT_STAMP_AT(4);  // task posting, iteration prologue, Philox
-        // barrier A; also the block-wide exit test (every wave runs every barrier):
-        // a wave with an active lane raises this step's flag (xcnt[par*2+1],
-        // cleared for the other parity after the barrier) — one s_barrier,
-        // where __syncthreads_or costs three
-        {
-            const uint64_t am = __ballot(active);
-            if (am && lane == __ffsll((long long)am) - 1) xcnt[par * 2 + 1] = 1;
-        }
-        __syncthreads();
-        if (xcnt[par * 2 + 1] == 0) break;
-        IPT_STAMP_AT(5);  // barrier A
-        if (tid == 0) {
-            xcnt[(1 - par) * 2 + 0] = 0;
-            xcnt[(1 - par) * 2 + 1] = 0;
-        }
-        {
-            // frame passes dealt round-robin to the 4 waves; results go straight
-            // into the requesting lane's frame column
-            const int nf = min(xcnt[par * 2 + 0], kFrameSlots);
-            for (int sl = wave * 64 + lane; sl < ((nf + 63) & ~63); sl += kBlock) {
-                if (sl < nf) {
-                    IPT_PHASE(5);
-                    const vec3 nn = normalize(v3(xfr[0 * kFrameSlots + sl], xfr[1 * kFrameSlots + sl],
-                                                 xfr[2 * kFrameSlots + sl]));
-                    const int col = __float_as_int(xfr[3 * kFrameSlots + sl]);
-                    const Frame f = make_frame(nn);
-                    if (IPT_ABL == 1) keep_alive(make_frame(nn * (1.0f + kp.abl_zero)));
-                    float* c = lfr + col;
-                    c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
-                    c[3 * kFrameStride] = f.m1.x; c[4 * kFrameStride] = f.m1.y; c[5 * kFrameStride] = f.m1.z;
-                    c[6 * kFrameStride] = f.m2.x; c[7 * kFrameStride] = f.m2.y; c[8 * kFrameStride] = f.m2.z;
-                    c[9 * kFrameStride] = f.iz.x; c[10 * kFrameStride] = f.iz.y; c[11 * kFrameStride] = f.iz.z;
-                }
-            }
-        }
-        IPT_STAMP_AT(6);  // worker passes (frames, cosine samples)
-        __syncthreads();  // barrier B: results visible
-        IPT_STAMP_AT(7);  // barrier B
-        if (want_frame && !stalled) {
-            need_frame = false;
-            fdepth = tdepth;
-        }
+        // the wave's exit test (waves are independent after the setup barrier)
+        if (!__ballot(active)) break;
+        IPT_STAMP_AT(5);
         // the current node's frame: its wall column or the lane's own column
         const float* frc = lfr + (tkind < 5 ? kBlock + tkind : tid);
 
@@ -975,7 +918,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 is_iter = true;
             }
         }
-        ++step;
         IPT_STAMP_AT(8);  // direction
         // --------------------------------------------- phase 4: trace + resolve
         // the child's value (main.cpp:100-143) from its traces, then push it,
