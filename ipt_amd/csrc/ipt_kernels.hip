@@ -725,33 +725,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
 
         IPT_STAMP_AT(2);  // finalize + pop
         IPT_STAMP_AT(3);  // (new path: later in the step)
-        // ------------- phase 3: the current node's RotateDdf frame when it is a sphere node without one
-        // (after a push, or a pop past a sphere descendant): built by the lane
-        // itself into its LDS column. Waves share no LDS after the setup, so they
-        // run without barriers (a pooled workgroup frame pass with two barriers
-        // per step measured 5-13 % slower).
-        if (need_frame && has_path && !fresh && !((kRes || kResL) && tracing)) {
-            vec3 nrm;
-            if (GEOM == IPT_GEOM_SPHERE_IN_BOX || tkind == 5) {
-                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67
-            } else {
-                const float4 sp = kp.spheres[tkind - 6];
-                nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
-                // GeometrySmallPt.cpp:41: -normalize(v) for the room spheres;
-                // normalize(-v) is the same bits (negation is exact)
-                if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
-            }
-            IPT_PHASE(5);
-            const Frame f = make_frame(normalize(nrm));
-            if (IPT_ABL == 1) keep_alive(make_frame(normalize(nrm * (1.0f + kp.abl_zero))));
-            float* c = lfr + tid;
-            c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
-            c[3 * kFrameStride] = f.m1.x; c[4 * kFrameStride] = f.m1.y; c[5 * kFrameStride] = f.m1.z;
-            c[6 * kFrameStride] = f.m2.x; c[7 * kFrameStride] = f.m2.y; c[8 * kFrameStride] = f.m2.z;
-            c[9 * kFrameStride] = f.iz.x; c[10 * kFrameStride] = f.iz.y; c[11 * kFrameStride] = f.iz.z;
-            need_frame = false;
-            fdepth = tdepth;
-        }
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
         const bool iter_lane = active && has_path && !fresh && !((kRes || kResL) && tracing);
         int pick = -1;
@@ -811,6 +784,34 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
             }
+        }
+        // (the frame build sits between the table gathers' issue and their use)
+        // ------------- phase 3: the current node's RotateDdf frame when it is a sphere node without one
+        // (after a push, or a pop past a sphere descendant): built by the lane
+        // itself into its LDS column. Waves share no LDS after the setup, so they
+        // run without barriers (a pooled workgroup frame pass with two barriers
+        // per step measured 5-13 % slower).
+        if (need_frame && has_path && !fresh && !((kRes || kResL) && tracing)) {
+            vec3 nrm;
+            if (GEOM == IPT_GEOM_SPHERE_IN_BOX || tkind == 5) {
+                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67
+            } else {
+                const float4 sp = kp.spheres[tkind - 6];
+                nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
+                // GeometrySmallPt.cpp:41: -normalize(v) for the room spheres;
+                // normalize(-v) is the same bits (negation is exact)
+                if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
+            }
+            IPT_PHASE(5);
+            const Frame f = make_frame(normalize(nrm));
+            if (IPT_ABL == 1) keep_alive(make_frame(normalize(nrm * (1.0f + kp.abl_zero))));
+            float* c = lfr + tid;
+            c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
+            c[3 * kFrameStride] = f.m1.x; c[4 * kFrameStride] = f.m1.y; c[5 * kFrameStride] = f.m1.z;
+            c[6 * kFrameStride] = f.m2.x; c[7 * kFrameStride] = f.m2.y; c[8 * kFrameStride] = f.m2.z;
+            c[9 * kFrameStride] = f.iz.x; c[10 * kFrameStride] = f.iz.y; c[11 * kFrameStride] = f.iz.z;
+            need_frame = false;
+            fdepth = tdepth;
         }
         if (IPT_PROF && wave == 0) { IPT_PHASE(11); }  // workgroup steps (one wave counts)
         IPT_STAMP_AT(4);  // task posting, iteration prologue, Philox
