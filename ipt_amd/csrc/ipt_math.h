@@ -497,16 +497,30 @@ IPT_HD void mulhilo32(uint32_t a, uint32_t b, uint32_t* hi, uint32_t* lo) {
     *hi = (uint32_t)(p >> 32);
     *lo = (uint32_t)p;
 }
+// a ^ b ^ c: one v_bitop3_b32 (truth table 0x96) on gfx950
+IPT_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
 IPT_HD u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                            uint32_t k1) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the round keys are two scalar adds each: keep them in the loop, where
+    // they cost SALU slots, instead of hoisted and spilled to VGPR lanes
+    // (every reload a v_readlane + hazard nops on the VALU)
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         uint32_t hi0, lo0, hi1, lo1;
         mulhilo32(M0, c0, &hi0, &lo0);
         mulhilo32(M1, c2, &hi1, &lo1);
-        uint32_t n0 = hi1 ^ c1 ^ k0;
-        uint32_t n2 = hi0 ^ c3 ^ k1;
+        uint32_t n0 = xor3(hi1, c1, k0);
+        uint32_t n2 = xor3(hi0, c3, k1);
         c0 = n0;
         c1 = lo1;
         c2 = n2;
