@@ -44,6 +44,9 @@ namespace {
 constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOCK for experiments)
 
 // Micro-optimisation switches (all exact; 0 restores the plain form, for A/B builds)
+#ifndef IPT_LV
+#define IPT_LV 3  // single light: its P, x, y, n, inv held in VGPRs (bit mask; +3.5 % C2)
+#endif
 #ifndef IPT_NL1
 #define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
 #endif
@@ -190,6 +193,12 @@ __device__ __forceinline__ bool longer_sq(float x, float y) {
     return r;
 }
 __device__ __forceinline__ bool longer(vec3 a, vec3 b) { return longer_sq(dot(a, a), dot(b, b)); }
+
+// A uniform value kept in a VGPR (the asm output counts as divergent), so
+// that its uses read it directly instead of from an SGPR spilled to a VGPR
+// lane (v_readlane + hazard nops per use).
+__device__ __forceinline__ void vgpr_hold(float& f) { asm volatile("" : "+v"(f)); }
+__device__ __forceinline__ void vgpr_hold(vec3& v) { vgpr_hold(v.x); vgpr_hold(v.y); vgpr_hold(v.z); }
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
     if (kp.n_shards <= 1 || kp.tile_rows <= 0) return true;
@@ -598,6 +607,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     LS.cg = kp.cdf;
     if (LMODE == kLightsOne) {
         LS.one = kp.lights[0];
+        if (IPT_LV & 1) { vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y); }
+        if (IPT_LV & 2) { vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]); }
+        if (IPT_LV & 4) { vgpr_hold(LS.one.area); vgpr_hold(LS.one.spow); }
         LS.w0 = kp.weights[0];
         LS.c0 = kp.cdf[0];
         LS.c1 = kp.cdf[1];
