@@ -47,6 +47,9 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_LV
 #define IPT_LV 3  // single light: its P, x, y, n, inv held in VGPRs (bit mask; +3.5 % C2)
 #endif
+#ifndef IPT_LVG
+#define IPT_LVG 1  // sphere grid: its geometry parameters held in VGPRs (+5 % C3)
+#endif
 #ifndef IPT_NL1
 #define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
 #endif
@@ -199,6 +202,7 @@ __device__ __forceinline__ bool longer(vec3 a, vec3 b) { return longer_sq(dot(a,
 // lane (v_readlane + hazard nops per use).
 __device__ __forceinline__ void vgpr_hold(float& f) { asm volatile("" : "+v"(f)); }
 __device__ __forceinline__ void vgpr_hold(vec3& v) { vgpr_hold(v.x); vgpr_hold(v.y); vgpr_hold(v.z); }
+__device__ __forceinline__ void vgpr_hold(int& i) { asm volatile("" : "+v"(i)); }
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
     if (kp.n_shards <= 1 || kp.tile_rows <= 0) return true;
@@ -615,6 +619,17 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         LS.c1 = kp.cdf[1];
     }
 
+    // the sphere grid walk's parameters (kRes instances)
+    KParams kg = kp;
+    if (IPT_LVG && resumable_geom(GEOM)) {
+        for (int a = 0; a < 3; ++a) {
+            vgpr_hold(kg.grid_g0[a]);
+            vgpr_hold(kg.grid_h[a]);
+            vgpr_hold(kg.grid_n[a]);
+        }
+        vgpr_hold(kg.grid_m);
+        vgpr_hold(kg.bvh_tmargin);
+    }
     const int lane = tid & 63;
     const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int nl = (IPT_NL1 && LMODE == kLightsOne) ? 1 : kp.n_lights;
@@ -1190,7 +1205,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (GEOM == IPT_GEOM_SPHERES_IN_BOX)
                     xbest = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(ro, rd, &xp)
                                                            : trace_box_planes_only<false>(ro, rd, &xp);
-                if (kp.n_grid > 0) sphere_grid_init(kp, ro, rd, xi, xtm);
+                if (kp.n_grid > 0) sphere_grid_init(kg, ro, rd, xi, xtm);
                 tracing = true;
             } else {
                 int prim = -1;
@@ -1212,7 +1227,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             IPT_PHASE(9);
             bool done;
             if (kp.n_grid > 0) {
-                sphere_grid_walk<COUNT>(kp, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET, c_nodes, c_tests);
+                sphere_grid_walk<COUNT>(kg, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET, c_nodes, c_tests);
                 done = xi < 0;
             } else {
                 sphere_bvh_walk<COUNT>(kp, xro, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
