@@ -102,6 +102,11 @@ constexpr int kProfPhases = 12;
         const uint64_t pm_ = __ballot(1);              \
         prof_w[id] += 1u;                              \
         prof_l[id] += (uint32_t)__popcll(pm_);         \
+    }                                                  \
+    if (IPT_MARK_PHASES) {                             \
+        __builtin_amdgcn_sched_barrier(0);             \
+        asm volatile(";@PHASE " #id);                  \
+        __builtin_amdgcn_sched_barrier(0);             \
     }
 
 // Diagnostic stamp builds (-DIPT_STAMP=1, scripts/prof_phases.sh): wave-cycles
@@ -109,6 +114,12 @@ constexpr int kProfPhases = 12;
 // SHARES (the stamps' waits forbid overlaps the real kernel has).
 #ifndef IPT_STAMP
 #define IPT_STAMP 0
+#endif
+#ifndef IPT_MARK_PHASES
+#define IPT_MARK_PHASES 0  // asm-listing builds: a ;@PHASE comment at each IPT_PHASE
+#endif
+#ifndef IPT_MARK
+#define IPT_MARK 0  // asm-listing builds: a ;@STAMP comment at each stamp (scripts/seg_insts.py)
 #endif
 constexpr int kStamps = 12;
 #define IPT_STAMP_AT(id)                                                                   \
@@ -119,6 +130,11 @@ constexpr int kStamps = 12;
         __builtin_amdgcn_sched_barrier(0);                                                 \
         st_acc[id] += (uint32_t)(t_ - st_last);                                            \
         st_last = t_;                                                                      \
+    }                                                                                      \
+    if (IPT_MARK) {                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        asm volatile(";@STAMP " #id);                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
     }
 template <typename T>
 __device__ __forceinline__ void keep_alive(const T& v) {

@@ -102,9 +102,23 @@ IPT_HD vec3 cosine_sample_local(float u1, float u2) {
 // 1 - sgn*oa is 0 or in [2^-24, 2^40) (1 - oa is exact near 1) and the divisor
 // in [1e-6, 2): the range-free division is exact (div_inrange_); a zero
 // numerator gives t = +-0, rejected below either way.
+// IPT_BRANCHFREE: the early returns of the plane / sphere / area-light tests
+// become one select over every test (same comparisons, same arithmetic, so
+// the same result for every input incl. NaN); in a wave that mixes passing
+// and failing lanes the branches only cost exec-mask bookkeeping.
+#ifndef IPT_BRANCHFREE
+#define IPT_BRANCHFREE 1  // +3.3 % C2
+#endif
 template <bool INRANGE = false>
 IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
     const float dp = sgn * da;
+    if (IPT_BRANCHFREE) {
+        const float t = INRANGE ? div_inrange_(1.0f - sgn * oa, dp) : div_(1.0f - sgn * oa, dp);
+        const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
+        const bool miss = lt_1em6(fabs_(dp)) | (fabs_(px) > 1.0f) | (fabs_(py) > 1.0f) | (fabs_(pz) > 1.0f) |
+                          (dp < 0.0f) | lt_1em6(t);
+        return miss ? inf_() : t;
+    }
     if (lt_1em6(fabs_(dp))) return inf_();
     const float t = INRANGE ? div_inrange_(1.0f - sgn * oa, dp) : div_(1.0f - sgn * oa, dp);
     const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
@@ -121,6 +135,18 @@ IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
 IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
     const float b = dot(o, d);
     const float desc = 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
+    if (IPT_BRANCHFREE) {
+        const float sd = sqrt_(desc);
+        const float m2b = -2.0f * b;
+        float t1 = (m2b - sd) * 0.5f;
+        float t2 = (m2b + sd) * 0.5f;
+        t1 = lt_1em6(t1) ? inf_() : t1;
+        t2 = lt_1em6(t2) ? inf_() : t2;
+        const float t = (t2 < t1) ? t2 : t1;
+        const vec3 pos = o + d * t;
+        const bool back = dot(pos, o - pos) <= 0.0f;
+        return (desc < 0.0f) ? inf_() : ((t == inf_()) ? t : (back ? inf_() : t));
+    }
     if (desc < 0.0f) return inf_();
     const float sd = sqrt_(desc);
     const float m2b = -2.0f * b;
@@ -227,6 +253,17 @@ IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* nrm)
         return true;
     }
     const float n_dir = dot(L.n, d);
+    if (IPT_BRANCHFREE) {
+        const float t = div_(dot(L.n, L.P - o), n_dir);
+        const vec3 rel = (o + d * t) - L.P;
+        const vec3 coord = mul(L.inv, rel);
+        const bool in = L.type == 0
+                            ? (coord.x >= 0.0f) & (coord.x <= 1.0f) & (coord.y >= 0.0f) & (coord.y <= 1.0f)
+                            : (coord.x >= 0.0f) & (coord.y >= 0.0f) & (coord.x + coord.y <= 1.0f);
+        *hit = L.P + rel;
+        *nrm = L.n;
+        return !(lt_1em6(fabs_(n_dir)) | (n_dir > 0.0f)) & !lt_1em6(t) & in;
+    }
     if (lt_1em6(fabs_(n_dir)) || n_dir > 0.0f) return false;
     const float t = div_(dot(L.n, L.P - o), n_dir);
     if (lt_1em6(t)) return false;
