@@ -50,6 +50,9 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_LVG
 #define IPT_LVG 1  // sphere grid: its geometry parameters held in VGPRs (+5 % C3)
 #endif
+#ifndef IPT_BFRESOLVE
+#define IPT_BFRESOLVE 1  // resolve's hit/light/expand decision as selects (+1 %)
+#endif
 #ifndef IPT_NL1
 #define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
 #endif
@@ -971,7 +974,34 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             float cv = 0.0f;
             bool push = false;
             vec3 si_pos = v3(0, 0, 0);
-            if (traced) {
+            if (IPT_BFRESOLVE) {
+                // the same decisions as below as selects (the branches only
+                // cost exec-mask bookkeeping in waves that mix outcomes)
+                const bool has_si = prim >= 0;
+                if (COUNT && traced) {
+                    ++c_traced;
+                    c_surf += has_si ? 1u : 0u;
+                    c_light += has_li ? 1u : 0u;
+                }
+                si_pos = o + d * t;
+                const vec3 ea = si_pos - o, eb = li_pos - o;
+                const float x = dot(ea, ea), y = dot(eb, eb);
+                // longer(si_pos - o, li_pos - o), asked only where both hits exist
+                const bool need = has_li && has_si;
+                bool lg = x > y * 1.000001907f && y >= 1e-30f;
+                if (!IPT_LENCMP) lg = false;
+                const bool tie = need && (!IPT_LENCMP || (!lg && !(x <= y)));
+                if (__builtin_expect(__any(tie), 0))
+                    if (tie) lg = sqrt_(x) > sqrt_(y);
+                const bool li_wins = has_li && (!has_si || lg);
+                const int nchild = kp.n_rays >> depth;
+                const float zero = 0.0f;
+                const float cv_exp = nchild == 0 ? zero / (float)nchild : 0.0f;
+                cv = li_wins ? (isfinite_(li_pow) ? li_pow : 1.0f) : (has_si ? cv_exp : 0.0f);
+                cv = traced ? cv : 0.0f;
+                push = traced && !li_wins && has_si && nchild != 0;
+                if (COUNT && traced && !li_wins && has_si) ++c_exp;
+            } else if (traced) {
                 const bool has_si = prim >= 0;
                 if (COUNT) {
                     ++c_traced;

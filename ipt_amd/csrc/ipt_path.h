@@ -106,6 +106,9 @@ IPT_HD vec3 cosine_sample_local(float u1, float u2) {
 // become one select over every test (same comparisons, same arithmetic, so
 // the same result for every input incl. NaN); in a wave that mixes passing
 // and failing lanes the branches only cost exec-mask bookkeeping.
+#ifndef IPT_BFPDF
+#define IPT_BFPDF 1  // light_pdf's facing test as a select
+#endif
 #ifndef IPT_BRANCHFREE
 #define IPT_BRANCHFREE 1  // +3.3 % C2
 #endif
@@ -286,6 +289,12 @@ IPT_HD float light_pdf(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nrm) 
     if (!has) return 0.0f;
     const vec3 dir = normalize(hit - o);
     const float cosinus = dot(nrm, -dir);
+    if (IPT_BFPDF) {
+        const vec3 ho = hit - o;
+        const float decay = dot(ho, ho);
+        const float p = div_(div_(decay, cosinus), L.area);
+        return cosinus < 0.0f ? 0.0f : p;
+    }
     if (cosinus < 0.0f) return 0.0f;
     const vec3 ho = hit - o;
     const float decay = dot(ho, ho);
