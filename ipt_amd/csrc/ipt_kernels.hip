@@ -188,6 +188,7 @@ struct KParams {
     int box_inrange;                      // camera and sphere list within 2^39 (box_plane_t<true>)
     const float* __restrict__ cos_a;      // [2^24] CosineDdf table by u1's 24 bits: sin(acos(sqrt(u1)))
     const float2* __restrict__ cos_b;     // [2^24] by u2's 24 bits: (cos phi, sin phi)
+    const float2* __restrict__ frame_sc;  // frame_table_kernel: RotateDdf angle (sin, cos) by to.z
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
@@ -222,6 +223,38 @@ __device__ __forceinline__ bool longer(vec3 a, vec3 b) { return longer_sq(dot(a,
 __device__ __forceinline__ void vgpr_hold(float& f) { asm volatile("" : "+v"(f)); }
 __device__ __forceinline__ void vgpr_hold(vec3& v) { vgpr_hold(v.x); vgpr_hold(v.y); vgpr_hold(v.z); }
 __device__ __forceinline__ void vgpr_hold(int& i) { asm volatile("" : "+v"(i)); }
+
+#ifndef IPT_FRAME_CALL
+#define IPT_FRAME_CALL 0
+#endif
+#ifndef IPT_FRAME_INRANGE
+#define IPT_FRAME_INRANGE 1  // +1.4 % C2
+#endif
+// the exact RotateDdf frame as a called function: its f64 polynomial constants
+// and temporaries then occupy registers only inside the call
+__device__ __attribute__((noinline)) Frame make_frame_call(vec3 to) { return make_frame(to); }
+
+// The RotateDdf angle's (sin, cos) are functions of to.z alone: an exact
+// table over every float with |to.z| in [2^-8, 1] (frame_table_kernel, 1 GiB),
+// entry ((bits(|z|) - bits(2^-8)) << 1 | sign); other z (|z| < 2^-8, NaN) are
+// computed. Replaces the f64 acos + sincos of most frame builds by one gather.
+constexpr uint32_t kFrameTabLo = 0x3b800000u;    // 2^-8
+constexpr uint32_t kFrameTabSpan = 0x04000000u;  // bits(1.0) - bits(2^-8)
+constexpr size_t kFrameTabEntries = 2 * ((size_t)kFrameTabSpan + 1);
+#ifndef IPT_FRAME_TAB
+#define IPT_FRAME_TAB 1  // +8.6 % C2
+#endif
+__device__ __forceinline__ void frame_sc_lookup(const float2* __restrict__ tab, vec3 to, float& s, float& c) {
+    const uint32_t u = f2u(to.z), m = u & 0x7fffffffu;
+    const bool in = m - kFrameTabLo <= kFrameTabSpan;
+    if (in) {
+        const float2 e = tab[((m - kFrameTabLo) << 1) | (u >> 31)];
+        s = e.x;
+        c = e.y;
+    }
+    if (__builtin_expect(__any(!in), 0))
+        if (!in) frame_angle_sc(to, &s, &c);
+}
 
 __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
     if (kp.n_shards <= 1 || kp.tile_rows <= 0) return true;
@@ -849,7 +882,34 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
             }
             IPT_PHASE(5);
-            const Frame f = make_frame(normalize(nrm));
+            Frame f;
+            if (IPT_ABL == 9) {
+                // profiling only (not the reference's frame): a trig-free basis
+                // with the same third column, i.e. the same sample distribution
+                const vec3 n = normalize(nrm);
+                const float sg = n.z >= 0.0f ? 1.0f : -1.0f;
+                const float a = -1.0f / (sg + n.z), b = n.x * n.y * a;
+                f.m0 = v3(1.0f + sg * n.x * n.x * a, sg * b, -sg * n.x);
+                f.m1 = v3(b, sg + n.y * n.y * a, -n.y);
+                f.m2 = n;
+                f.iz = n;
+            } else {
+                // the sphere-in-box node's normal comes from a point on the
+                // r = 0.5 sphere: every root and quotient of the frame is in the
+                // range-free sequences' range (make_frame<true>)
+                constexpr bool kFrameInrange = IPT_FRAME_INRANGE && GEOM == IPT_GEOM_SPHERE_IN_BOX;
+                if (IPT_FRAME_CALL)
+                    f = make_frame_call(normalize(nrm));
+                else if (IPT_FRAME_TAB) {
+                    const vec3 to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                    float fs = 0.0f, fc = 0.0f;
+                    frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                    f = make_frame_sc<kFrameInrange>(to, fs, fc);
+                } else if (kFrameInrange)
+                    f = make_frame<true>(normalize_inrange_(nrm));
+                else
+                    f = make_frame(normalize(nrm));
+            }
             if (IPT_ABL == 1) keep_alive(make_frame(normalize(nrm * (1.0f + kp.abl_zero))));
             float* c = lfr + tid;
             c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
@@ -1453,6 +1513,14 @@ __device__ __host__ inline float math_fn(int fn, float x) {
             const uint32_t d = udiv_pair_d(f2u(x));
             return u2f(udiv_exact(f2u(x), d, 1.0 / (double)d));
         }
+        case 13:  // the range-free root on its range [2^-96, 2^126), sqrtf elsewhere
+            return (x >= 0x1p-96f && x < 0x1p126f) ? sqrt_inrange_(x) : sqrt_(x);
+        case 14:
+        case 15: {  // the RotateDdf angle's sin / cos for to.z = x
+            float sv, cv;
+            frame_angle_sc(v3(0.6f, 0.8f, x), &sv, &cv);
+            return fn == 14 ? sv : cv;
+        }
         case 0: return acosf_(x);
         case 1: return sinf_(x);
         case 2: return cosf_(x);
@@ -1545,6 +1613,18 @@ __global__ void cos_table_kernel(float* __restrict__ a, float2* __restrict__ b) 
     b[i] = make_float2(cp, sp);
 }
 
+// frame_sc table (frame_sc_lookup): entry i is frame_angle_sc of to.z = the
+// float with |bits| = kFrameTabLo + (i >> 1) and sign i & 1 (dot((0,0,1), to)
+// is to.z for finite to.x, to.y and to.z != 0).
+__global__ void frame_table_kernel(float2* __restrict__ t) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kFrameTabEntries) return;
+    const float z = u2f((kFrameTabLo + (uint32_t)(i >> 1)) | ((uint32_t)(i & 1) << 31));
+    float sv, cv;
+    frame_angle_sc(v3(0.0f, 0.0f, z), &sv, &cv);
+    t[i] = make_float2(sv, cv);
+}
+
 // Exact restatement of math_fn (differs only where the device uses a fast
 // path, i.e. fn 3): the reference for ipt_math_selfcheck.
 __device__ float math_fn_exact(int fn, float x) {
@@ -1557,17 +1637,24 @@ __device__ float math_fn_exact(int fn, float x) {
         return sqrt_(a) > sqrt_(b) ? 1.0f : 0.0f;  // glm length comparison as written
     }
     if (fn == 12) return u2f(f2u(x) / udiv_pair_d(f2u(x)));
+    if (fn == 13) return __builtin_sqrtf(x);  // IEEE (compiler sequence)
     return math_fn(fn, x);
 }
 
 __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long long n,
-                                 unsigned long long* bad, unsigned int* first) {
+                                 unsigned long long* bad, unsigned int* first, const float2* __restrict__ ftab) {
     unsigned long long local = 0;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
     for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t b = (uint32_t)(lo + i);
         const float x = u2f(b);
-        const float a = math_fn(fn, x), e = math_fn_exact(fn, x);
+        float a = math_fn(fn, x);
+        const float e = math_fn_exact(fn, x);
+        if (fn == 14 || fn == 15) {  // the path kernel's table lookup (frame_sc_lookup)
+            float sv = 0.0f, cv = 0.0f;
+            frame_sc_lookup(ftab, v3(0.6f, 0.8f, x), sv, cv);
+            a = fn == 14 ? sv : cv;
+        }
         // fn 10: a zero quotient's sign is not observed by the callers
         if (!(f2u(a) == f2u(e) || (a != a && e != e) || (fn == 10 && a == 0.0f && e == 0.0f))) {
             ++local;
@@ -1627,6 +1714,7 @@ struct ipt_ctx {
     float* d_cos_a = nullptr;   // CosineDdf tables (cos_table_kernel): r 64 MiB,
                                 // (cos phi, sin phi) 128 MiB
     float2* d_cos_b = nullptr;
+    float2* d_frame_sc = nullptr;  // frame_table_kernel (IPT_FRAME_TAB), 1 GiB
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
     int blocks_per_cu = 0;
@@ -1656,6 +1744,15 @@ int ensure_cos_tables(ipt_ctx* ctx, hipStream_t st) {
     HIPCHECK(ctx, hipMalloc(&ctx->d_cos_a, n * sizeof(float)));
     HIPCHECK(ctx, hipMalloc(&ctx->d_cos_b, n * sizeof(float2)));
     hipLaunchKernelGGL(cos_table_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, st, ctx->d_cos_a, ctx->d_cos_b);
+    HIPCHECK(ctx, hipGetLastError());
+    return IPT_OK;
+}
+
+int ensure_frame_table(ipt_ctx* ctx, hipStream_t st) {
+    if (!IPT_FRAME_TAB || ctx->d_frame_sc) return IPT_OK;
+    HIPCHECK(ctx, hipMalloc(&ctx->d_frame_sc, kFrameTabEntries * sizeof(float2)));
+    hipLaunchKernelGGL(frame_table_kernel, dim3((unsigned)((kFrameTabEntries + 255) / 256)), dim3(256), 0, st,
+                       ctx->d_frame_sc);
     HIPCHECK(ctx, hipGetLastError());
     return IPT_OK;
 }
@@ -1812,6 +1909,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     if (rc) return rc;
     rc = ensure_cos_tables(ctx, st);
     if (rc) return rc;
+    rc = ensure_frame_table(ctx, st);
+    if (rc) return rc;
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice, st));
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice, st));
     const int susp = needed_susp(p);
@@ -1879,6 +1978,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cdf_bsearch = ctx->cdf_bsearch;
         kp.cos_a = ctx->d_cos_a;
         kp.cos_b = ctx->d_cos_b;
+        kp.frame_sc = ctx->d_frame_sc;
         kp.cand_lds = (p->n_shards > 1 && p->tile_rows > 0 && kp.n_cand <= kLdsCand) ? 1 : 0;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
@@ -1988,7 +2088,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
-                    ctx->d_grid_start, ctx->d_grid_items};
+                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_frame_sc};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& e : ctx->ev)
@@ -2267,7 +2367,7 @@ int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms) {
 }
 
 int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
-    if (!in || !out || n < 0 || fn < 0 || fn > 12) return IPT_E_INVALID;
+    if (!in || !out || n < 0 || fn < 0 || fn > 15) return IPT_E_INVALID;
     const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t)
@@ -2279,7 +2379,7 @@ int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
 }
 
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n) {
-    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 12) return IPT_E_INVALID;
+    if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 15) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     float *din = nullptr, *dout = nullptr;
     HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * 4));
@@ -2346,9 +2446,14 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
                        uint32_t* first_bad) {
-    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 12 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 15 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
         return IPT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (fn == 14 || fn == 15) {
+        if (!IPT_FRAME_TAB) return fail(ctx, IPT_E_INVALID, "ipt_math_selfcheck: built without the frame table");
+        const int rc = ensure_frame_table(ctx, ctx->stream);
+        if (rc) return rc;
+    }
     unsigned long long* d_bad = nullptr;
     unsigned int* d_first = nullptr;
     HIPCHECK(ctx, hipMalloc(&d_bad, sizeof(unsigned long long)));
@@ -2358,7 +2463,7 @@ int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits,
     const unsigned long long n = hi_bits - lo_bits;
     if (n > 0)
         hipLaunchKernelGGL(selfcheck_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, ctx->stream, fn,
-                           (unsigned long long)lo_bits, n, d_bad, d_first);
+                           (unsigned long long)lo_bits, n, d_bad, d_first, ctx->d_frame_sc);
     HIPCHECK(ctx, hipGetLastError());
     unsigned long long hb = 0;
     unsigned int hf = 0;

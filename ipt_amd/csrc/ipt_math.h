@@ -39,6 +39,23 @@ IPT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 IPT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 IPT_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
 IPT_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
+// An f64 constant of the frame / sampling polynomials, materialised where it
+// is used (two SALU moves): left to the compiler, they are hoisted out of the
+// path loop and, as SGPR pairs live across it, push the loop's other uniform
+// values into spill lanes (the exact RotateDdf frame's ~30 constants cost C2
+// more than all of its arithmetic).
+#ifndef IPT_KD
+#define IPT_KD 0
+#endif
+IPT_HD double kd_(uint64_t u) {
+    double v = __builtin_bit_cast(double, u);
+#if defined(__HIP_DEVICE_COMPILE__) && IPT_KD == 1
+    asm volatile("" : "+s"(v));
+#elif defined(__HIP_DEVICE_COMPILE__) && IPT_KD == 2
+    asm volatile("" : "+v"(v));
+#endif
+    return v;
+}
 
 IPT_HD float fabs_(float x) { return u2f(f2u(x) & 0x7fffffffu); }
 IPT_HD bool isfinite_(float x) { return (f2u(x) & 0x7f800000u) != 0x7f800000u; }
@@ -118,6 +135,23 @@ IPT_HD float div_inrange_(float a, float b) {
 #endif
 }
 
+// Correctly rounded sqrtf for x in [2^-96, 2^126): the hardware root (within
+// one ulp, no denormal scaling needed in this range) corrected by the signs of
+// the residuals of its two neighbours (the sequence of the IEEE expansion
+// without its range handling). Equal to sqrtf on every float of the range
+// (exhaustive GPU check, math probe 13).
+IPT_HD float sqrt_inrange_(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = u2f(f2u(s) - 1u), su = u2f(f2u(s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    const float s1 = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : s1;
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+
 // ------------------------------------------------------------------ vec3
 // glm::vec3 with glm's component-wise operators; no FMA anywhere.
 struct vec3 {
@@ -147,6 +181,13 @@ IPT_HD vec3 normalize(vec3 v) {
     return v * s;
 }
 
+// normalize for dot(v, v) in [2^-80, 2^80] (root in [2^-40, 2^40]): the same
+// roundings as normalize() through the range-free root and quotient
+IPT_HD vec3 normalize_inrange_(vec3 v) {
+    const float s = div_inrange_(1.0f, sqrt_inrange_(dot(v, v)));
+    return v * s;
+}
+
 // column-major mat3, m[c][r] as glm
 struct mat3 {
     vec3 c[3];
@@ -162,6 +203,7 @@ IPT_HD float el(const mat3& m, int c, int r) {
     return r == 0 ? v.x : (r == 1 ? v.y : v.z);
 }
 // glm compute_inverse<3,3> (func_matrix.inl:268-291), cofactor / determinant
+template <bool INRANGE = false>
 IPT_HD mat3 inverse(const mat3& M) {
     const float m00 = M.c[0].x, m01 = M.c[0].y, m02 = M.c[0].z;
     const float m10 = M.c[1].x, m11 = M.c[1].y, m12 = M.c[1].z;
@@ -170,7 +212,7 @@ IPT_HD mat3 inverse(const mat3& M) {
     det = det - m10 * (m01 * m22 - m21 * m02);
     det = det + m20 * (m01 * m12 - m11 * m02);
     // glm writes "+ m00*(..) - m10*(..) + m20*(..)"; unary + is exact
-    const float o = div_(1.0f, det);
+    const float o = INRANGE ? div_inrange_(1.0f, det) : div_(1.0f, det);  // INRANGE: det in [2^-40, 2^41)
     mat3 I;
     I.c[0].x = (m11 * m22 - m21 * m12) * o;
     I.c[1].x = -(m10 * m22 - m20 * m12) * o;
@@ -233,13 +275,13 @@ IPT_HD sincos_tab sincos_table(int which) {
     sincos_tab t;
     const double sg = which ? -1.0 : 1.0;
     t.c0 = sg * 1.0;
-    t.c1 = sg * u2d(0xbfdffffffd0c621cull);
-    t.s1 = u2d(0xbfc555545995a603ull);
-    t.c2 = sg * u2d(0x3fa55553e1068f19ull);
-    t.s2 = u2d(0x3f81107605230bc4ull);
-    t.c3 = sg * u2d(0xbf56c087e89a359dull);
-    t.s3 = u2d(0xbf2994eb3774cf24ull);
-    t.c4 = sg * u2d(0x3ef99343027bf8c3ull);
+    t.c1 = sg * kd_(0xbfdffffffd0c621cull);
+    t.s1 = kd_(0xbfc555545995a603ull);
+    t.c2 = sg * kd_(0x3fa55553e1068f19ull);
+    t.s2 = kd_(0x3f81107605230bc4ull);
+    t.c3 = sg * kd_(0xbf56c087e89a359dull);
+    t.s3 = kd_(0xbf2994eb3774cf24ull);
+    t.c4 = sg * kd_(0x3ef99343027bf8c3ull);
     return t;
 }
 IPT_HD double sincos_sign(int q) { return (q == 1 || q == 2) ? -1.0 : 1.0; }
@@ -289,11 +331,11 @@ IPT_HD double reduce_large_(uint32_t xi, int* np) {
 
 // fast reduction: n = round(x*2/pi) via (int)(x*hpi_inv*2^24) + 2^23 >> 24; x - n*hpi (one FMA)
 IPT_HD double reduce_fast_(double x, int* np) {
-    const double hpi_inv = u2d(0x41645f306dc9c883ull);  // 0x1.45f306dc9c883p+23
+    const double hpi_inv = kd_(0x41645f306dc9c883ull);  // 0x1.45f306dc9c883p+23
     double r = x * hpi_inv;
     int n = ((int32_t)r + 0x800000) >> 24;
     *np = n;
-    return fma_(-(double)n, u2d(0x3ff921fb54442d18ull), x);
+    return fma_(-(double)n, kd_(0x3ff921fb54442d18ull), x);
 }
 
 IPT_HD void sincosf_small_(float y, float* sp, float* cp);
@@ -377,14 +419,14 @@ IPT_HD float sinf_small_(float y) {
 // equality of that rounding with glibc's acos for all float inputs in [-1,1]
 // is checked exhaustively in tests/test_math_exhaustive.py.
 IPT_HD double acos_d_(double x) {
-    const double pi = u2d(0x400921fb54442d18ull);
-    const double pio2_hi = u2d(0x3ff921fb54442d18ull);
-    const double pio2_lo = u2d(0x3c91a62633145c07ull);
-    const double pS0 = u2d(0x3fc5555555555555ull), pS1 = u2d(0xbfd4d61203eb6f7dull),
-                 pS2 = u2d(0x3fc9c1550e884455ull), pS3 = u2d(0xbfa48228b5688f3bull),
-                 pS4 = u2d(0x3f49efe07501b288ull), pS5 = u2d(0x3f023de10dfdf709ull);
-    const double qS1 = u2d(0xc0033a271c8a2d4bull), qS2 = u2d(0x40002ae59c598ac8ull),
-                 qS3 = u2d(0xbfe6066c1b8d0159ull), qS4 = u2d(0x3fb3b8c5b12e9282ull);
+    const double pi = kd_(0x400921fb54442d18ull);
+    const double pio2_hi = kd_(0x3ff921fb54442d18ull);
+    const double pio2_lo = kd_(0x3c91a62633145c07ull);
+    const double pS0 = kd_(0x3fc5555555555555ull), pS1 = kd_(0xbfd4d61203eb6f7dull),
+                 pS2 = kd_(0x3fc9c1550e884455ull), pS3 = kd_(0xbfa48228b5688f3bull),
+                 pS4 = kd_(0x3f49efe07501b288ull), pS5 = kd_(0x3f023de10dfdf709ull);
+    const double qS1 = kd_(0xc0033a271c8a2d4bull), qS2 = kd_(0x40002ae59c598ac8ull),
+                 qS3 = kd_(0xbfe6066c1b8d0159ull), qS4 = kd_(0x3fb3b8c5b12e9282ull);
     const uint64_t hx64 = d2u(x);
     const uint32_t hx = (uint32_t)(hx64 >> 32);
     const uint32_t ix = hx & 0x7fffffffu;
@@ -427,14 +469,14 @@ IPT_HD float acos_f64_to_f32(float xf) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double x = (double)xf;
     const double ax = __builtin_fabs(x);
-    const double pi = u2d(0x400921fb54442d18ull);
-    const double pio2_hi = u2d(0x3ff921fb54442d18ull);
-    const double pio2_lo = u2d(0x3c91a62633145c07ull);
-    const double pS0 = u2d(0x3fc5555555555555ull), pS1 = u2d(0xbfd4d61203eb6f7dull),
-                 pS2 = u2d(0x3fc9c1550e884455ull), pS3 = u2d(0xbfa48228b5688f3bull),
-                 pS4 = u2d(0x3f49efe07501b288ull), pS5 = u2d(0x3f023de10dfdf709ull);
-    const double qS1 = u2d(0xc0033a271c8a2d4bull), qS2 = u2d(0x40002ae59c598ac8ull),
-                 qS3 = u2d(0xbfe6066c1b8d0159ull), qS4 = u2d(0x3fb3b8c5b12e9282ull);
+    const double pi = kd_(0x400921fb54442d18ull);
+    const double pio2_hi = kd_(0x3ff921fb54442d18ull);
+    const double pio2_lo = kd_(0x3c91a62633145c07ull);
+    const double pS0 = kd_(0x3fc5555555555555ull), pS1 = kd_(0xbfd4d61203eb6f7dull),
+                 pS2 = kd_(0x3fc9c1550e884455ull), pS3 = kd_(0xbfa48228b5688f3bull),
+                 pS4 = kd_(0x3f49efe07501b288ull), pS5 = kd_(0x3f023de10dfdf709ull);
+    const double qS1 = kd_(0xc0033a271c8a2d4bull), qS2 = kd_(0x40002ae59c598ac8ull),
+                 qS3 = kd_(0xbfe6066c1b8d0159ull), qS4 = kd_(0x3fb3b8c5b12e9282ull);
     const bool small = ax < 0.5;
     const double z = small ? x * x : (1.0 - ax) * 0.5;
     const double p = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
@@ -460,7 +502,7 @@ IPT_HD float acos_f64_to_f32(float xf) {
         A = pi - 2.0 * (sg + (r * sg - pio2_lo));
     else
         A = 2.0 * (sg + r * sg);
-    const double d = u2d(0x3d30000000000000ull);  // 2^-44
+    const double d = kd_(0x3d30000000000000ull);  // 2^-44
     const float lo = (float)(A * (1.0 - d)), hi = (float)(A * (1.0 + d));
     if (lo == hi && ax < 1.0) return lo;
     return (float)acos_d_(x);

@@ -34,15 +34,39 @@ struct Frame {
 
 // RotateDdf constructor (ddf_detail.h:73-84) incl. glm::rotate
 // (ext/matrix_transform.inl:18-47) applied to identity and mat3(mat4).
-IPT_HD Frame make_frame(vec3 to) {
+// INRANGE: `to` has unit length up to rounding (a normalized vector), so the
+// axis test, both roots and both quotients (|axis| = 1 or >= 1e-6, det ~ 1)
+// take the range-free sequences (same roundings, see sqrt_inrange_).
+// glm::rotate's cos(a), sin(a) of a = (float)acos((double)dot(z, to))
+// (ddf_detail.h:82), a in [0, pi]
+IPT_HD void frame_angle_sc(vec3 to, float* s, float* c) {
+    const float cosinus = dot(v3(0.0f, 0.0f, 1.0f), to);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(IPT_ABL) && (IPT_ABL == 11 || IPT_ABL == 13)
+    const float a = acosf(cosinus);  // profiling only: not the reference's rounding
+#else
+    const float a = acos_f64_to_f32(cosinus);
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(IPT_ABL) && (IPT_ABL == 12 || IPT_ABL == 13)
+    *s = __sinf(a); *c = __cosf(a);  // profiling only
+#else
+    sincosf_small_(a, s, c);
+#endif
+}
+// The frame from `to` and the angle's (s, c) (make_frame below, or an exact
+// table of frame_angle_sc by to.z's bits in the path kernel).
+template <bool INRANGE = false>
+IPT_HD Frame make_frame_sc(vec3 to, float s, float c) {
     const vec3 z = v3(0.0f, 0.0f, 1.0f);
     vec3 axis = cross(z, to);
-    if (lt_1em6(length(axis))) axis = v3(1.0f, 0.0f, 0.0f);
-    const float cosinus = dot(z, to);
-    const float a = acos_f64_to_f32(cosinus);
-    float s, c;
-    sincosf_small_(a, &s, &c);  // glm::rotate's cos(a), sin(a); a in [0,pi]
-    const vec3 ax = normalize(axis);
+    if (INRANGE) {
+        // length(axis) < 1e-6 is certain below 2^-80 (root 2^-40), where the
+        // range-free root is not used
+        const float q = dot(axis, axis);
+        if ((q < 0x1p-80f) | lt_1em6(sqrt_inrange_(q))) axis = v3(1.0f, 0.0f, 0.0f);
+    } else {
+        if (lt_1em6(length(axis))) axis = v3(1.0f, 0.0f, 0.0f);
+    }
+    const vec3 ax = INRANGE ? normalize_inrange_(axis) : normalize(axis);
     const vec3 temp = (1.0f - c) * ax;
     float R[3][3];
     R[0][0] = c + temp.x * ax.x;
@@ -62,13 +86,19 @@ IPT_HD Frame make_frame(vec3 to) {
         float e2 = (0.0f * R[k][0] + 0.0f * R[k][1]) + 1.0f * R[k][2];
         M.c[k] = v3(e0, e1, e2);
     }
-    const mat3 I = inverse(M);
+    const mat3 I = inverse<INRANGE>(M);
     Frame f;
     f.m0 = M.c[0];
     f.m1 = M.c[1];
     f.m2 = M.c[2];
     f.iz = v3(I.c[0].z, I.c[1].z, I.c[2].z);
     return f;
+}
+template <bool INRANGE = false>
+IPT_HD Frame make_frame(vec3 to) {
+    float s, c;
+    frame_angle_sc(to, &s, &c);
+    return make_frame_sc<INRANGE>(to, s, c);
 }
 IPT_HD vec3 frame_apply(const Frame& f, vec3 v) {
     return v3(f.m0.x * v.x + f.m1.x * v.y + f.m2.x * v.z,

@@ -111,7 +111,7 @@ def test_cli_render_matches_oracle(gpu_ctx, oracle, tmp_path):
 
 
 @pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs", "div_inrange_pairs", "longer_pairs",
-                                "udiv_exact_pairs"])
+                                "udiv_exact_pairs", "sqrt_inrange", "frame_angle_sin", "frame_angle_cos"])
 def test_fast_math_exhaustive(gpu_ctx, fn):
     """The device fast paths equal their exact references on all 2^32 inputs:
     (float)acos((double)x) (Ziv test + exact fallback) vs the fdlibm
@@ -121,7 +121,11 @@ def test_fast_math_exhaustive(gpu_ctx, fn):
     range-free division of the box planes (div_inrange_) over the same pairs;
     the squares-first length comparison (longer_sq) against sqrtf(x) >
     sqrtf(y) over 2^32 near-tie and unrelated pairs; the 32-bit work-unit
-    decomposition (udiv_exact) against integer division over 2^32 pairs."""
+    decomposition (udiv_exact) against integer division over 2^32 pairs; the
+    range-free root (frame builds) against sqrtf on its range; the frame
+    table's (sin, cos) of the RotateDdf angle, looked up by to.z's bits,
+    against the computed angle for every float z (incl. the table's ends
+    2^-8 and 1, the computed |z| < 2^-8 and NaN)."""
     bad, first = gpu_ctx.math_selfcheck(capi.MATH_FNS[fn])
     assert bad == 0, (fn, bad, hex(first))
 
