@@ -103,8 +103,10 @@ constexpr int kProfPhases = 12;
 #define IPT_PHASE(id)                                  \
     if (IPT_PROF) {                                    \
         const uint64_t pm_ = __ballot(1);              \
-        prof_w[id] += 1u;                              \
-        prof_l[id] += (uint32_t)__popcll(pm_);         \
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)pm_) - 1) { \
+            prof_w[id] += 1u;                          \
+            prof_l[id] += (uint32_t)__popcll(pm_);     \
+        }                                              \
     }                                                  \
     if (IPT_MARK_PHASES) {                             \
         __builtin_amdgcn_sched_barrier(0);             \
@@ -803,6 +805,22 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }
 
         IPT_STAMP_AT(2);  // finalize + pop
+        // the current node's frame normal (frame build below)
+        auto frame_normal = [&]() -> vec3 {
+            vec3 nrm;
+            if (GEOM == IPT_GEOM_SPHERE_IN_BOX || tkind == 5) {
+                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67
+            } else {
+                const float4 sp = kp.spheres[tkind - 6];
+                nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
+                // GeometrySmallPt.cpp:41: -normalize(v) for the room spheres;
+                // normalize(-v) is the same bits (negation is exact)
+                if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
+            }
+            return nrm;
+        };
+        constexpr bool kFrameInrange = IPT_FRAME_INRANGE && GEOM == IPT_GEOM_SPHERE_IN_BOX;
+        const bool fneed = need_frame && has_path && !fresh && !((kRes || kResL) && tracing);
         IPT_STAMP_AT(3);  // (new path: later in the step)
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
         const bool iter_lane = active && has_path && !fresh && !((kRes || kResL) && tracing);
@@ -870,17 +888,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // itself into its LDS column. Waves share no LDS after the setup, so they
         // run without barriers (a pooled workgroup frame pass with two barriers
         // per step measured 5-13 % slower).
-        if (need_frame && has_path && !fresh && !((kRes || kResL) && tracing)) {
-            vec3 nrm;
-            if (GEOM == IPT_GEOM_SPHERE_IN_BOX || tkind == 5) {
-                nrm = tpos;  // normalize(position), GeometrySphereInBox.cpp:67
-            } else {
-                const float4 sp = kp.spheres[tkind - 6];
-                nrm = tpos - v3(sp.x, sp.y, sp.z);  // FractalSpheres.cpp:91
-                // GeometrySmallPt.cpp:41: -normalize(v) for the room spheres;
-                // normalize(-v) is the same bits (negation is exact)
-                if (GEOM == IPT_GEOM_SMALLPT && !((double)sp.w < 100.0)) nrm = -nrm;
-            }
+        if (fneed) {
+            const vec3 nrm = frame_normal();
             IPT_PHASE(5);
             Frame f;
             if (IPT_ABL == 9) {
@@ -897,7 +906,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // the sphere-in-box node's normal comes from a point on the
                 // r = 0.5 sphere: every root and quotient of the frame is in the
                 // range-free sequences' range (make_frame<true>)
-                constexpr bool kFrameInrange = IPT_FRAME_INRANGE && GEOM == IPT_GEOM_SPHERE_IN_BOX;
                 if (IPT_FRAME_CALL)
                     f = make_frame_call(normalize(nrm));
                 else if (IPT_FRAME_TAB) {
@@ -1351,11 +1359,13 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     if (IPT_STAMP && lane == 0)
         for (int q = 0; q < kStamps; ++q)
             atomicAdd(&kp.counters[kNumCounters + 2 * kProfPhases + q], (unsigned long long)st_acc[q]);
-    if (IPT_PROF && lane == 0)
-        for (int q = 0; q < kProfPhases; ++q) {
-            atomicAdd(&kp.counters[kNumCounters + 2 * q], (unsigned long long)prof_w[q]);
-            atomicAdd(&kp.counters[kNumCounters + 2 * q + 1], (unsigned long long)prof_l[q]);
-        }
+    // (each wave-execution of a phase was counted by its lowest active lane)
+    if (IPT_PROF)
+        for (int q = 0; q < kProfPhases; ++q)
+            if (prof_w[q]) {
+                atomicAdd(&kp.counters[kNumCounters + 2 * q], (unsigned long long)prof_w[q]);
+                atomicAdd(&kp.counters[kNumCounters + 2 * q + 1], (unsigned long long)prof_l[q]);
+            }
     if (COUNT) {
         atomicAdd(&kp.counters[0], (unsigned long long)c_paths);
         atomicAdd(&kp.counters[1], (unsigned long long)c_traced);
