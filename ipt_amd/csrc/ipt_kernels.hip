@@ -908,7 +908,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // range-free sequences' range (make_frame<true>)
                 if (IPT_FRAME_CALL)
                     f = make_frame_call(normalize(nrm));
-                else if (IPT_FRAME_TAB) {
+                else if (IPT_FRAME_TAB && GEOM == IPT_GEOM_SPHERE_IN_BOX) {
+                    // (sphere-list scenes: measured slower with the table's
+                    // gathers in their latency-bound walks)
                     const vec3 to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
                     float fs = 0.0f, fc = 0.0f;
                     frame_sc_lookup(kp.frame_sc, to, fs, fc);

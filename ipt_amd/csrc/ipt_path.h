@@ -165,10 +165,13 @@ IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
 // (float)((-2.0*b -+ sqrt_desc)/2.0) equals (-2b -+ sqrt_desc)*0.5f in f32:
 // both operands are floats, so the f64 difference is exact whenever it can
 // affect the f32 rounding (see DESIGN.md "mixed precision").
+// BF: branch-free (the box's one sphere, hit by a large share of rays); the
+// sphere lists' tests stay branchy (most miss at the discriminant)
+template <bool BF = false>
 IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
     const float b = dot(o, d);
     const float desc = 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
-    if (IPT_BRANCHFREE) {
+    if (BF) {
         const float sd = sqrt_(desc);
         const float m2b = -2.0f * b;
         float t1 = (m2b - sd) * 0.5f;
@@ -231,7 +234,7 @@ template <bool INRANGE = false>
 IPT_HD float trace_box(vec3 o, vec3 d, int* prim) {
     int bi;
     float best = trace_box_planes_only<INRANGE>(o, d, &bi);
-    const float ts = sphere_t(0.5f, o, d);
+    const float ts = sphere_t<IPT_BRANCHFREE>(0.5f, o, d);
     if (ts < best) { best = ts; bi = 5; }
     *prim = bi;
     return best;

@@ -14,7 +14,7 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv 
 python scripts/summarize_rocprof.py $T gpurun_out/stats_$T gpurun_out/fetch_$T gpurun_out/write_$T gpurun_out/stats_${T}_bench.json || exit 1
 timeout -k 10 600 python bench.py > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err || { echo "bench failed"; tail gpurun_out/bench_$T.err; exit 1; }
 for c in c3 c5; do
-  timeout -k 10 500 python bench.py --config $c --steps 1 --warmup 0 --cpu-seconds 0 > gpurun_out/bench_${T}_$c.json 2> gpurun_out/bench_${T}_$c.err || { echo "$c failed"; tail -5 gpurun_out/bench_${T}_$c.err; exit 1; }
+  timeout -k 10 500 python bench.py --config $c --steps 2 --warmup 1 --cpu-seconds 0 > gpurun_out/bench_${T}_$c.json 2> gpurun_out/bench_${T}_$c.err || { echo "$c failed"; tail -5 gpurun_out/bench_${T}_$c.err; exit 1; }
 done
 python - <<PY
 import json
