@@ -53,6 +53,9 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_BFRESOLVE
 #define IPT_BFRESOLVE 1  // resolve's hit/light/expand decision as selects (+1 %)
 #endif
+#ifndef IPT_POPMASK
+#define IPT_POPMASK 1  // multi-level pops from a per-lane finished-levels mask (+3 % C2)
+#endif
 #ifndef IPT_NL1
 #define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
 #endif
@@ -707,6 +710,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     Win8 w;
     vec3 tpos = v3(0, 0, 0);
     int fdepth = -1;  // depth of the sphere node whose frame is in the lane's column
+    uint32_t finm = 0;  // IPT_POPMASK: bit l = the node suspended at level l has run all its iterations
     // Resumable sphere-BVH walks (sphere-list scenes): a lane whose walk is not
     // done within IPT_WALK_BUDGET node visits keeps its ray and light results
     // and resumes the walk in the next steps (doing nothing else meanwhile), so
@@ -774,7 +778,41 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         IPT_STAMP_AT(1);  // refill
         if (active) { IPT_PHASE(0); }
         // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
-        if (active && has_path && !fresh && !((kRes || kResL) && tracing)) {
+        if (IPT_POPMASK && active && has_path && !fresh && !((kRes || kResL) && tracing) &&
+            ti >= (kp.n_rays >> tdepth)) {
+            // the node is done: unwind every suspended level whose node has run
+            // all its iterations too (finm, set at push) in one pass -- only
+            // their res/multiplier are read -- then resume the first level
+            // with iterations left (or store the path's value)
+            IPT_PHASE(1);
+            auto fin_v = [&](float r, int d) {
+                float v = 0.0f;
+                if (isfinite_(r))
+                    v = n_pow2 ? r * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - d)) : r / (float)(kp.n_rays >> d);
+                return v;
+            };
+            float v = fin_v(tres, tdepth);
+            const uint32_t m = ~finm & ((1u << tdepth) - 1u);
+            const int stop = m ? 31 - (int)__clz(m) : -1;
+            for (int l = tdepth - 1; l > stop; --l) {
+                const float* b = stk + (size_t)l * kStackFields * kBlock + tid;
+                v = fin_v(b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v, l);
+            }
+            if (stop < 0) {
+                kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
+                has_path = false;
+            } else {
+                const float* b = stk + (size_t)stop * kStackFields * kBlock + tid;
+                tpos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
+                const int meta = __float_as_int(b[5 * kBlock]);
+                tres = b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v;  // res += multiplier*albedo*ray_power
+                ti = meta & 0xff;
+                tkind = meta >> 8;
+                tdepth = stop;
+                need_frame = tkind >= 5 && fdepth != stop;
+            }
+        }
+        if (!IPT_POPMASK && active && has_path && !fresh && !((kRes || kResL) && tracing)) {
             for (;;) {
                 const int n = kp.n_rays >> tdepth;
                 if (ti < n) break;
@@ -1097,6 +1135,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             if (push) {
                 IPT_PHASE(10);
                 if (iter) {
+                    if (IPT_POPMASK)
+                        finm = (finm & ~(1u << tdepth)) | ((ti >= (kp.n_rays >> tdepth) ? 1u : 0u) << tdepth);
                     float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
                     b[0 * kBlock] = tpos.x;
                     b[1 * kBlock] = tpos.y;
