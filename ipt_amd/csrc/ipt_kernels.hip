@@ -907,8 +907,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     // (cos phi, sin phi) looked up by the draws' 24 bits; consumed after
                     // barrier B, so the loads' latency hides behind the frame pass
                     // (a non-temporal hint measured slower on C2 and C5)
-                    // (cos_alpha = sqrtf(u1) is recomputed in the direction phase:
-                    // the 64 MiB r table + the 128 MiB phi table gather less)
+                    // (cos_alpha = sqrtf(u1) is recomputed in the direction phase)
                     const float tr = kp.cos_a[r1 >> 8];
                     const float2 tb = kp.cos_b[r2 >> 8];
                     u2 = tr;
@@ -1059,7 +1058,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
                 // cosine_sample_local from the tables: (r cos phi, r sin phi, cos_alpha)
                 // with u2 = r and cos_alpha = sqrtf(u1)
-                dir = frame_apply(fm, v3(u2 * cs_c, u2 * cs_s, sqrt_(u1)));
+                // u1 is 0 or in [2^-24, 1): the range-free root is sqrtf there
+                // (math probe 13 is exhaustive on [2^-96, 2^126); sqrt_inrange_(0) = +0)
+                dir = frame_apply(fm, v3(u2 * cs_c, u2 * cs_s, sqrt_inrange_(u1)));
             }
             ++ti;
             if (COUNT) ++c_iter;
@@ -1565,8 +1566,8 @@ __device__ __host__ inline float math_fn(int fn, float x) {
             const uint32_t d = udiv_pair_d(f2u(x));
             return u2f(udiv_exact(f2u(x), d, 1.0 / (double)d));
         }
-        case 13:  // the range-free root on its range [2^-96, 2^126), sqrtf elsewhere
-            return (x >= 0x1p-96f && x < 0x1p126f) ? sqrt_inrange_(x) : sqrt_(x);
+        case 13:  // the range-free root on its range +0, [2^-96, 2^126); sqrtf elsewhere
+            return (f2u(x) == 0u || (x >= 0x1p-96f && x < 0x1p126f)) ? sqrt_inrange_(x) : sqrt_(x);
         case 14:
         case 15: {  // the RotateDdf angle's sin / cos for to.z = x
             float sv, cv;

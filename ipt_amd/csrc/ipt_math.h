@@ -135,7 +135,7 @@ IPT_HD float div_inrange_(float a, float b) {
 #endif
 }
 
-// Correctly rounded sqrtf for x in [2^-96, 2^126): the hardware root (within
+// Correctly rounded sqrtf for x = +0 or in [2^-96, 2^126): the hardware root (within
 // one ulp, no denormal scaling needed in this range) corrected by the signs of
 // the residuals of its two neighbours (the sequence of the IEEE expansion
 // without its range handling). Equal to sqrtf on every float of the range
