@@ -229,15 +229,9 @@ __device__ __forceinline__ void vgpr_hold(float& f) { asm volatile("" : "+v"(f))
 __device__ __forceinline__ void vgpr_hold(vec3& v) { vgpr_hold(v.x); vgpr_hold(v.y); vgpr_hold(v.z); }
 __device__ __forceinline__ void vgpr_hold(int& i) { asm volatile("" : "+v"(i)); }
 
-#ifndef IPT_FRAME_CALL
-#define IPT_FRAME_CALL 0
-#endif
 #ifndef IPT_FRAME_INRANGE
 #define IPT_FRAME_INRANGE 1  // +1.4 % C2
 #endif
-// the exact RotateDdf frame as a called function: its f64 polynomial constants
-// and temporaries then occupy registers only inside the call
-__device__ __attribute__((noinline)) Frame make_frame_call(vec3 to) { return make_frame(to); }
 
 // The RotateDdf angle's (sin, cos) are functions of to.z alone: an exact
 // table over every float with |to.z| in [2^-8, 1] (frame_table_kernel, 1 GiB),
@@ -943,9 +937,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // the sphere-in-box node's normal comes from a point on the
                 // r = 0.5 sphere: every root and quotient of the frame is in the
                 // range-free sequences' range (make_frame<true>)
-                if (IPT_FRAME_CALL)
-                    f = make_frame_call(normalize(nrm));
-                else if (IPT_FRAME_TAB && GEOM == IPT_GEOM_SPHERE_IN_BOX) {
+                if (IPT_FRAME_TAB && GEOM == IPT_GEOM_SPHERE_IN_BOX) {
                     // (sphere-list scenes: measured slower with the table's
                     // gathers in their latency-bound walks)
                     const vec3 to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);

@@ -39,23 +39,6 @@ IPT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 IPT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 IPT_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
 IPT_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
-// An f64 constant of the frame / sampling polynomials, materialised where it
-// is used (two SALU moves): left to the compiler, they are hoisted out of the
-// path loop and, as SGPR pairs live across it, push the loop's other uniform
-// values into spill lanes (the exact RotateDdf frame's ~30 constants cost C2
-// more than all of its arithmetic).
-#ifndef IPT_KD
-#define IPT_KD 0
-#endif
-IPT_HD double kd_(uint64_t u) {
-    double v = __builtin_bit_cast(double, u);
-#if defined(__HIP_DEVICE_COMPILE__) && IPT_KD == 1
-    asm volatile("" : "+s"(v));
-#elif defined(__HIP_DEVICE_COMPILE__) && IPT_KD == 2
-    asm volatile("" : "+v"(v));
-#endif
-    return v;
-}
 
 IPT_HD float fabs_(float x) { return u2f(f2u(x) & 0x7fffffffu); }
 IPT_HD bool isfinite_(float x) { return (f2u(x) & 0x7f800000u) != 0x7f800000u; }
@@ -275,13 +258,13 @@ IPT_HD sincos_tab sincos_table(int which) {
     sincos_tab t;
     const double sg = which ? -1.0 : 1.0;
     t.c0 = sg * 1.0;
-    t.c1 = sg * kd_(0xbfdffffffd0c621cull);
-    t.s1 = kd_(0xbfc555545995a603ull);
-    t.c2 = sg * kd_(0x3fa55553e1068f19ull);
-    t.s2 = kd_(0x3f81107605230bc4ull);
-    t.c3 = sg * kd_(0xbf56c087e89a359dull);
-    t.s3 = kd_(0xbf2994eb3774cf24ull);
-    t.c4 = sg * kd_(0x3ef99343027bf8c3ull);
+    t.c1 = sg * u2d(0xbfdffffffd0c621cull);
+    t.s1 = u2d(0xbfc555545995a603ull);
+    t.c2 = sg * u2d(0x3fa55553e1068f19ull);
+    t.s2 = u2d(0x3f81107605230bc4ull);
+    t.c3 = sg * u2d(0xbf56c087e89a359dull);
+    t.s3 = u2d(0xbf2994eb3774cf24ull);
+    t.c4 = sg * u2d(0x3ef99343027bf8c3ull);
     return t;
 }
 IPT_HD double sincos_sign(int q) { return (q == 1 || q == 2) ? -1.0 : 1.0; }
@@ -331,11 +314,11 @@ IPT_HD double reduce_large_(uint32_t xi, int* np) {
 
 // fast reduction: n = round(x*2/pi) via (int)(x*hpi_inv*2^24) + 2^23 >> 24; x - n*hpi (one FMA)
 IPT_HD double reduce_fast_(double x, int* np) {
-    const double hpi_inv = kd_(0x41645f306dc9c883ull);  // 0x1.45f306dc9c883p+23
+    const double hpi_inv = u2d(0x41645f306dc9c883ull);  // 0x1.45f306dc9c883p+23
     double r = x * hpi_inv;
     int n = ((int32_t)r + 0x800000) >> 24;
     *np = n;
-    return fma_(-(double)n, kd_(0x3ff921fb54442d18ull), x);
+    return fma_(-(double)n, u2d(0x3ff921fb54442d18ull), x);
 }
 
 IPT_HD void sincosf_small_(float y, float* sp, float* cp);
@@ -419,14 +402,14 @@ IPT_HD float sinf_small_(float y) {
 // equality of that rounding with glibc's acos for all float inputs in [-1,1]
 // is checked exhaustively in tests/test_math_exhaustive.py.
 IPT_HD double acos_d_(double x) {
-    const double pi = kd_(0x400921fb54442d18ull);
-    const double pio2_hi = kd_(0x3ff921fb54442d18ull);
-    const double pio2_lo = kd_(0x3c91a62633145c07ull);
-    const double pS0 = kd_(0x3fc5555555555555ull), pS1 = kd_(0xbfd4d61203eb6f7dull),
-                 pS2 = kd_(0x3fc9c1550e884455ull), pS3 = kd_(0xbfa48228b5688f3bull),
-                 pS4 = kd_(0x3f49efe07501b288ull), pS5 = kd_(0x3f023de10dfdf709ull);
-    const double qS1 = kd_(0xc0033a271c8a2d4bull), qS2 = kd_(0x40002ae59c598ac8ull),
-                 qS3 = kd_(0xbfe6066c1b8d0159ull), qS4 = kd_(0x3fb3b8c5b12e9282ull);
+    const double pi = u2d(0x400921fb54442d18ull);
+    const double pio2_hi = u2d(0x3ff921fb54442d18ull);
+    const double pio2_lo = u2d(0x3c91a62633145c07ull);
+    const double pS0 = u2d(0x3fc5555555555555ull), pS1 = u2d(0xbfd4d61203eb6f7dull),
+                 pS2 = u2d(0x3fc9c1550e884455ull), pS3 = u2d(0xbfa48228b5688f3bull),
+                 pS4 = u2d(0x3f49efe07501b288ull), pS5 = u2d(0x3f023de10dfdf709ull);
+    const double qS1 = u2d(0xc0033a271c8a2d4bull), qS2 = u2d(0x40002ae59c598ac8ull),
+                 qS3 = u2d(0xbfe6066c1b8d0159ull), qS4 = u2d(0x3fb3b8c5b12e9282ull);
     const uint64_t hx64 = d2u(x);
     const uint32_t hx = (uint32_t)(hx64 >> 32);
     const uint32_t ix = hx & 0x7fffffffu;
@@ -469,14 +452,14 @@ IPT_HD float acos_f64_to_f32(float xf) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double x = (double)xf;
     const double ax = __builtin_fabs(x);
-    const double pi = kd_(0x400921fb54442d18ull);
-    const double pio2_hi = kd_(0x3ff921fb54442d18ull);
-    const double pio2_lo = kd_(0x3c91a62633145c07ull);
-    const double pS0 = kd_(0x3fc5555555555555ull), pS1 = kd_(0xbfd4d61203eb6f7dull),
-                 pS2 = kd_(0x3fc9c1550e884455ull), pS3 = kd_(0xbfa48228b5688f3bull),
-                 pS4 = kd_(0x3f49efe07501b288ull), pS5 = kd_(0x3f023de10dfdf709ull);
-    const double qS1 = kd_(0xc0033a271c8a2d4bull), qS2 = kd_(0x40002ae59c598ac8ull),
-                 qS3 = kd_(0xbfe6066c1b8d0159ull), qS4 = kd_(0x3fb3b8c5b12e9282ull);
+    const double pi = u2d(0x400921fb54442d18ull);
+    const double pio2_hi = u2d(0x3ff921fb54442d18ull);
+    const double pio2_lo = u2d(0x3c91a62633145c07ull);
+    const double pS0 = u2d(0x3fc5555555555555ull), pS1 = u2d(0xbfd4d61203eb6f7dull),
+                 pS2 = u2d(0x3fc9c1550e884455ull), pS3 = u2d(0xbfa48228b5688f3bull),
+                 pS4 = u2d(0x3f49efe07501b288ull), pS5 = u2d(0x3f023de10dfdf709ull);
+    const double qS1 = u2d(0xc0033a271c8a2d4bull), qS2 = u2d(0x40002ae59c598ac8ull),
+                 qS3 = u2d(0xbfe6066c1b8d0159ull), qS4 = u2d(0x3fb3b8c5b12e9282ull);
     const bool small = ax < 0.5;
     const double z = small ? x * x : (1.0 - ax) * 0.5;
     const double p = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
@@ -502,7 +485,7 @@ IPT_HD float acos_f64_to_f32(float xf) {
         A = pi - 2.0 * (sg + (r * sg - pio2_lo));
     else
         A = 2.0 * (sg + r * sg);
-    const double d = kd_(0x3d30000000000000ull);  // 2^-44
+    const double d = u2d(0x3d30000000000000ull);  // 2^-44
     const float lo = (float)(A * (1.0 - d)), hi = (float)(A * (1.0 + d));
     if (lo == hi && ax < 1.0) return lo;
     return (float)acos_d_(x);

@@ -33,10 +33,9 @@ struct Frame {
 };
 
 // RotateDdf constructor (ddf_detail.h:73-84) incl. glm::rotate
-// (ext/matrix_transform.inl:18-47) applied to identity and mat3(mat4).
-// INRANGE: `to` has unit length up to rounding (a normalized vector), so the
-// axis test, both roots and both quotients (|axis| = 1 or >= 1e-6, det ~ 1)
-// take the range-free sequences (same roundings, see sqrt_inrange_).
+// (ext/matrix_transform.inl:18-47) applied to identity and mat3(mat4):
+// make_frame = frame_angle_sc + make_frame_sc.
+//
 // glm::rotate's cos(a), sin(a) of a = (float)acos((double)dot(z, to))
 // (ddf_detail.h:82), a in [0, pi]
 IPT_HD void frame_angle_sc(vec3 to, float* s, float* c) {
@@ -54,6 +53,9 @@ IPT_HD void frame_angle_sc(vec3 to, float* s, float* c) {
 }
 // The frame from `to` and the angle's (s, c) (make_frame below, or an exact
 // table of frame_angle_sc by to.z's bits in the path kernel).
+// INRANGE: `to` has unit length up to rounding (a normalized vector), so the
+// axis test, both roots and both quotients (|axis| = 1 or >= 1e-6, det ~ 1)
+// take the range-free sequences (same roundings, see sqrt_inrange_).
 template <bool INRANGE = false>
 IPT_HD Frame make_frame_sc(vec3 to, float s, float c) {
     const vec3 z = v3(0.0f, 0.0f, 1.0f);
