@@ -171,6 +171,9 @@ typedef struct ipt_ctx ipt_ctx;
 int ipt_abi_version(void);
 const char* ipt_last_error(ipt_ctx* ctx); /* ctx may be NULL (creation errors) */
 
+/* A context owns its stream and device buffers. The first render allocates its
+ * exact sampling tables once: CosineDdf 192 MiB and, for sphere-in-box scenes,
+ * the RotateDdf frame-angle table 1 GiB (freed by ipt_destroy). */
 int ipt_create(int hip_device, ipt_ctx** out);
 void ipt_destroy(ipt_ctx* ctx);
 

@@ -1954,8 +1954,10 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     if (rc) return rc;
     rc = ensure_cos_tables(ctx, st);
     if (rc) return rc;
-    rc = ensure_frame_table(ctx, st);
-    if (rc) return rc;
+    if (ctx->geometry_kind == IPT_GEOM_SPHERE_IN_BOX) {  // its only user (path_kernel)
+        rc = ensure_frame_table(ctx, st);
+        if (rc) return rc;
+    }
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice, st));
     HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice, st));
     const int susp = needed_susp(p);
