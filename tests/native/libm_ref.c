@@ -22,6 +22,16 @@ static float eval1(int fn, float x) {
         case 6: return sqrtf(x);
         case 7: return (float)((double)x / M_PI);
         case 8: return (float)(2 * M_PI * (double)x);
+        case 13: return sqrtf(x);
+        case 14:
+        case 15: {
+            /* RotateDdf: cosinus = dot((0,0,1), to) for to = (0.6, 0.8, x),
+             * a = (float)acos((double)cosinus) (ddf_detail.h:82), glm::rotate's
+             * cos(a), sin(a) (matrix_transform.inl:21-22) */
+            const float cosinus = (0.0f * 0.6f + 0.0f * 0.8f) + 1.0f * x;
+            const float a = (float)acos((double)cosinus);
+            return fn == 14 ? sinf(a) : cosf(a);
+        }
     }
     return 0.0f;
 }

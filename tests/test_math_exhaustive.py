@@ -93,3 +93,13 @@ def test_acos_double_rounded_to_float(libm):
 def test_mixed_precision_helpers(libm):
     sweep(libm, F["div_pi"], 0, 0x40000001)  # CosineDdf::value z/M_PI in f64
     sweep(libm, F["sqrtf"], 0, 0x7f800000)
+
+
+def test_frame_angle_and_range_free_root(libm):
+    """Host build of the RotateDdf angle's (sin, cos) (the frame table's
+    entries, ipt_path.h frame_angle_sc) against glibc, and the range-free root
+    probe against sqrtf (its fast sequence is proven on the GPU)."""
+    for fn in ("frame_angle_sin", "frame_angle_cos"):
+        sweep(libm, F[fn], 0, 0x3f800001)
+        sweep(libm, F[fn], 0x80000000, 0xbf800001)
+    sweep(libm, F["sqrt_inrange"], 0, 0x7f800000)
