@@ -60,15 +60,20 @@ template <bool INRANGE = false>
 IPT_HD Frame make_frame_sc(vec3 to, float s, float c) {
     const vec3 z = v3(0.0f, 0.0f, 1.0f);
     vec3 axis = cross(z, to);
+    vec3 ax;
     if (INRANGE) {
         // length(axis) < 1e-6 is certain below 2^-80 (root 2^-40), where the
-        // range-free root is not used
+        // range-free root is not used; normalize(axis) reuses the root (the
+        // replacement (1,0,0) has dot 1 and root 1)
         const float q = dot(axis, axis);
-        if ((q < 0x1p-80f) | lt_1em6(sqrt_inrange_(q))) axis = v3(1.0f, 0.0f, 0.0f);
+        const float r = sqrt_inrange_(q);
+        const bool rep = (q < 0x1p-80f) | lt_1em6(r);
+        axis = rep ? v3(1.0f, 0.0f, 0.0f) : axis;
+        ax = axis * div_inrange_(1.0f, rep ? 1.0f : r);
     } else {
         if (lt_1em6(length(axis))) axis = v3(1.0f, 0.0f, 0.0f);
+        ax = normalize(axis);
     }
-    const vec3 ax = INRANGE ? normalize_inrange_(axis) : normalize(axis);
     const vec3 temp = (1.0f - c) * ax;
     float R[3][3];
     R[0][0] = c + temp.x * ax.x;
