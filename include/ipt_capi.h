@@ -177,14 +177,20 @@ const char* ipt_last_error(ipt_ctx* ctx); /* ctx may be NULL (creation errors) *
 int ipt_create(int hip_device, ipt_ctx** out);
 void ipt_destroy(ipt_ctx* ctx);
 
-/* Copies the scene (caller keeps ownership of its arrays). */
+/* Copies the scene (caller keeps ownership of its arrays). Transactional: on
+   any failure (IPT_E_OOM, IPT_E_DEVICE, ...) the context is left with NO
+   scene, so a later render returns IPT_E_NOSCENE instead of rendering a
+   half-uploaded one; upload again to recover. */
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* scene);
 
 /* Host buffers: copies the image in, renders p->spp passes, copies it out. */
 int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* host_img);
 
-/* Device buffers (hipMalloc'd or torch CUDA tensors) on `hip_stream`
-   (NULL = the context's own stream). Asynchronous w.r.t. the host. */
+/* Device buffers (hipMalloc'd or torch CUDA tensors), kernels launched on
+   `hip_stream` (NULL = the context's own stream) after the work already queued
+   there. Synchronous: the call returns when the image is complete (it waits
+   for the path and accumulate kernels of every chunk; ipt_last_kernel_ms then
+   holds their times). */
 int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, void* hip_stream);
 
 /* Per-sample radiance, for bit-exact verification: values[s][iy][ix] is the

@@ -13,4 +13,22 @@ int ctx_fail(ipt_ctx* ctx, int code, const std::string& msg);  // records ipt_la
 hipStream_t ctx_stream(ipt_ctx* ctx);
 int ctx_device(ipt_ctx* ctx);
 int ctx_cus(ipt_ctx* ctx);
+
+// Owning device allocation: a call's temporaries are freed on every return
+// path, early error returns included; release() hands the pointer over.
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    T* release() {
+        T* q = p;
+        p = nullptr;
+        return q;
+    }
+};
 }  // namespace ipt_internal

@@ -27,6 +27,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/ipt_capi.h"
@@ -1780,41 +1781,63 @@ int fail(ipt_ctx* ctx, int code, const std::string& msg) {
     do {                                                                                \
         hipError_t e_ = (expr);                                                         \
         if (e_ != hipSuccess)                                                           \
-            return fail(ctx, IPT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? IPT_E_OOM : IPT_E_DEVICE,      \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));             \
     } while (0)
 
+using ipt_internal::DevBuf;
+
+// The exact sampling tables are built once per context. Each is published in
+// the context only after its allocation, its build kernel and that kernel's
+// completion all succeeded, so a failure leaves no half-built table behind.
 int ensure_cos_tables(ipt_ctx* ctx, hipStream_t st) {
-    if (ctx->d_cos_a) return IPT_OK;
+    if (ctx->d_cos_a && ctx->d_cos_b) return IPT_OK;
     const size_t n = (size_t)1 << 24;
-    HIPCHECK(ctx, hipMalloc(&ctx->d_cos_a, n * sizeof(float)));
-    HIPCHECK(ctx, hipMalloc(&ctx->d_cos_b, n * sizeof(float2)));
-    hipLaunchKernelGGL(cos_table_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, st, ctx->d_cos_a, ctx->d_cos_b);
+    DevBuf<float> a;
+    DevBuf<float2> b;
+    HIPCHECK(ctx, hipMalloc(&a.p, n * sizeof(float)));
+    HIPCHECK(ctx, hipMalloc(&b.p, n * sizeof(float2)));
+    hipLaunchKernelGGL(cos_table_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, st, a.p, b.p);
     HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipStreamSynchronize(st));
+    ctx->d_cos_a = a.release();
+    ctx->d_cos_b = b.release();
     return IPT_OK;
 }
 
 int ensure_frame_table(ipt_ctx* ctx, hipStream_t st) {
     if (!IPT_FRAME_TAB || ctx->d_frame_sc) return IPT_OK;
-    HIPCHECK(ctx, hipMalloc(&ctx->d_frame_sc, kFrameTabEntries * sizeof(float2)));
-    hipLaunchKernelGGL(frame_table_kernel, dim3((unsigned)((kFrameTabEntries + 255) / 256)), dim3(256), 0, st,
-                       ctx->d_frame_sc);
+    DevBuf<float2> t;
+    HIPCHECK(ctx, hipMalloc(&t.p, kFrameTabEntries * sizeof(float2)));
+    hipLaunchKernelGGL(frame_table_kernel, dim3((unsigned)((kFrameTabEntries + 255) / 256)), dim3(256), 0, st, t.p);
     HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipStreamSynchronize(st));
+    ctx->d_frame_sc = t.release();
     return IPT_OK;
 }
 
+// Work buffers grow on demand. A buffer's capacity is dropped to 0 together
+// with the buffer, so a failed regrowth never leaves a stale capacity over a
+// null pointer.
 int ensure_work(ipt_ctx* ctx, size_t elems, size_t npix, int H, int n_cand) {
     if (elems > ctx->work_cap) {
         if (ctx->d_values) hipFree(ctx->d_values);
         if (ctx->d_codes) hipFree(ctx->d_codes);
         ctx->d_values = nullptr;
         ctx->d_codes = nullptr;
-        HIPCHECK(ctx, hipMalloc(&ctx->d_values, elems * sizeof(float)));
-        HIPCHECK(ctx, hipMalloc(&ctx->d_codes, elems));
+        ctx->work_cap = 0;
+        DevBuf<float> v;
+        DevBuf<uint8_t> c;
+        HIPCHECK(ctx, hipMalloc(&v.p, elems * sizeof(float)));
+        HIPCHECK(ctx, hipMalloc(&c.p, elems));
+        ctx->d_values = v.release();
+        ctx->d_codes = c.release();
         ctx->work_cap = elems;
     }
     if (npix > ctx->flags_cap) {
         if (ctx->d_flags) hipFree(ctx->d_flags);
         ctx->d_flags = nullptr;
+        ctx->flags_cap = 0;
         HIPCHECK(ctx, hipMalloc(&ctx->d_flags, npix));
         ctx->flags_cap = npix;
     }
@@ -1823,8 +1846,12 @@ int ensure_work(ipt_ctx* ctx, size_t elems, size_t npix, int H, int n_cand) {
         if (ctx->d_cand_of_row) hipFree(ctx->d_cand_of_row);
         ctx->d_cand_rows = nullptr;
         ctx->d_cand_of_row = nullptr;
-        HIPCHECK(ctx, hipMalloc(&ctx->d_cand_rows, sizeof(int) * std::max(n_cand, 1)));
-        HIPCHECK(ctx, hipMalloc(&ctx->d_cand_of_row, sizeof(int) * std::max(H, 1)));
+        ctx->cand_cap_rows = ctx->cand_cap_h = 0;
+        DevBuf<int> r, o;
+        HIPCHECK(ctx, hipMalloc(&r.p, sizeof(int) * std::max(n_cand, 1)));
+        HIPCHECK(ctx, hipMalloc(&o.p, sizeof(int) * std::max(H, 1)));
+        ctx->d_cand_rows = r.release();
+        ctx->d_cand_of_row = o.release();
         ctx->cand_cap_rows = n_cand;
         ctx->cand_cap_h = H;
     }
@@ -2236,59 +2263,72 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     bool cdf_mono = true;
     for (int i = 0; i <= nl; ++i)
         if (!(cdf[i] == cdf[i]) || (i > 0 && !(cdf[i - 1] <= cdf[i]))) cdf_mono = false;
-    void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes,
-                   ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items};
+    // Device phase, transactional: every buffer of the new scene is allocated
+    // and filled in a temporary first. Until all of them succeeded the context
+    // has no scene (renders fail with IPT_E_NOSCENE, never launch on a
+    // half-built one); on success the old buffers are freed and the new ones
+    // swapped in. IPT_TEST_FAIL_UPLOAD_ALLOC=k makes the k-th allocation of an
+    // upload fail (tests/test_gpu_parity.py exercises the failure path).
+    ctx->has_scene = false;
+    int n_alloc = 0;
+    int fail_at = 0;
+    if (const char* e = std::getenv("IPT_TEST_FAIL_UPLOAD_ALLOC")) fail_at = std::atoi(e);
+    auto upload = [&](auto& buf, const auto* src, size_t count) -> int {
+        using T = std::remove_pointer_t<decltype(buf.p)>;
+        if (++n_alloc == fail_at) return fail(ctx, IPT_E_OOM, "injected allocation failure (IPT_TEST_FAIL_UPLOAD_ALLOC)");
+        HIPCHECK(ctx, hipMalloc(&buf.p, sizeof(T) * std::max<size_t>(count, 1)));
+        if (count) HIPCHECK(ctx, hipMemcpy(buf.p, src, sizeof(T) * count, hipMemcpyHostToDevice));
+        return IPT_OK;
+    };
+    DevBuf<int> n_grid_start;
+    DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
+    DevBuf<BvhNode> n_light_nodes, n_bvh_nodes;
+    DevBuf<LightDev> n_lights;
+    DevBuf<float> n_weights, n_cdf;
+    DevBuf<float4> n_spheres;
+    DevBuf<Frame> n_wall;
+    int rc = IPT_OK;
+    if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
+    if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
+    if (!lnodes.empty() && !rc) rc = upload(n_light_nodes, lnodes.data(), lnodes.size());
+    if (!bnodes.empty() && !rc) rc = upload(n_bvh_nodes, bnodes.data(), bnodes.size());
+    if (!bnodes.empty() && !rc) rc = upload(n_bvh_prims, bprims.data(), bprims.size());
+    if (!rc) rc = upload(n_lights, L.data(), L.size());
+    if (!rc) rc = upload(n_weights, wts.data(), (size_t)nl + 1);
+    if (!rc) rc = upload(n_cdf, cdf.data(), (size_t)nl + 1);
+    if (!rc) rc = upload(n_wall, wall, 5);
+    if (!rc) rc = upload(n_spheres, sph.data(), sph.size());
+    if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
+    void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
+                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_wall};
     for (void* b : old)
         if (b) hipFree(b);
-    ctx->d_lights = nullptr;
-    ctx->d_weights = ctx->d_cdf = nullptr;
-    ctx->d_spheres = nullptr;
-    ctx->d_bvh_nodes = nullptr;
-    ctx->d_bvh_prims = nullptr;
-    ctx->n_nodes = 0;
-    ctx->d_light_nodes = nullptr;
-    ctx->n_light_nodes = 0;
-    ctx->d_grid_start = nullptr;
-    ctx->d_grid_items = nullptr;
+    ctx->d_grid_start = n_grid_start.release();
+    ctx->d_grid_items = n_grid_items.release();
     ctx->n_grid = 0;
     if (use_grid) {
-        HIPCHECK(ctx, hipMalloc(&ctx->d_grid_start, sizeof(int) * grid.start.size()));
-        HIPCHECK(ctx, hipMalloc(&ctx->d_grid_items, sizeof(BvhSphere) * std::max<size_t>(1, grid.items.size())));
-        HIPCHECK(ctx, hipMemcpy(ctx->d_grid_start, grid.start.data(), sizeof(int) * grid.start.size(), hipMemcpyHostToDevice));
-        if (!grid.items.empty())
-            HIPCHECK(ctx, hipMemcpy(ctx->d_grid_items, grid.items.data(), sizeof(BvhSphere) * grid.items.size(),
-                                    hipMemcpyHostToDevice));
         ctx->n_grid = (int)(grid.start.size() - 1);
         ctx->bvh_tmargin = grid.tmargin;
         grid.start.clear();
         grid.items.clear();
         ctx->grid = grid;
     }
-    if (!lnodes.empty()) {
-        HIPCHECK(ctx, hipMalloc(&ctx->d_light_nodes, sizeof(BvhNode) * lnodes.size()));
-        HIPCHECK(ctx, hipMemcpy(ctx->d_light_nodes, lnodes.data(), sizeof(BvhNode) * lnodes.size(),
-                                hipMemcpyHostToDevice));
-        ctx->n_light_nodes = n_lnodes;
-    }
+    ctx->d_light_nodes = n_light_nodes.release();
+    ctx->n_light_nodes = lnodes.empty() ? 0 : n_lnodes;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
     ctx->any_round_light = any_round;
+    ctx->d_bvh_nodes = n_bvh_nodes.release();
+    ctx->d_bvh_prims = n_bvh_prims.release();
+    ctx->n_nodes = 0;
     if (!bnodes.empty()) {
-        HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_nodes, sizeof(BvhNode) * bnodes.size()));
-        HIPCHECK(ctx, hipMalloc(&ctx->d_bvh_prims, sizeof(BvhSphere) * bprims.size()));
-        HIPCHECK(ctx, hipMemcpy(ctx->d_bvh_nodes, bnodes.data(), sizeof(BvhNode) * bnodes.size(), hipMemcpyHostToDevice));
-        HIPCHECK(ctx, hipMemcpy(ctx->d_bvh_prims, bprims.data(), sizeof(BvhSphere) * bprims.size(), hipMemcpyHostToDevice));
         ctx->n_nodes = per_order;  // nodes per octant order; buffer holds kBvhOrders of them
         ctx->bvh_tmargin = tmargin;
     }
-    HIPCHECK(ctx, hipMalloc(&ctx->d_lights, sizeof(LightDev) * L.size()));
-    HIPCHECK(ctx, hipMalloc(&ctx->d_weights, sizeof(float) * (nl + 1)));
-    HIPCHECK(ctx, hipMalloc(&ctx->d_cdf, sizeof(float) * (nl + 1)));
-    HIPCHECK(ctx, hipMalloc(&ctx->d_spheres, sizeof(float4) * sph.size()));
-    HIPCHECK(ctx, hipMemcpy(ctx->d_lights, L.data(), sizeof(LightDev) * L.size(), hipMemcpyHostToDevice));
-    HIPCHECK(ctx, hipMemcpy(ctx->d_weights, wts.data(), sizeof(float) * (nl + 1), hipMemcpyHostToDevice));
-    HIPCHECK(ctx, hipMemcpy(ctx->d_cdf, cdf.data(), sizeof(float) * (nl + 1), hipMemcpyHostToDevice));
-    HIPCHECK(ctx, hipMemcpy(ctx->d_wall, wall, sizeof(Frame) * 5, hipMemcpyHostToDevice));
-    HIPCHECK(ctx, hipMemcpy(ctx->d_spheres, sph.data(), sizeof(float4) * sph.size(), hipMemcpyHostToDevice));
+    ctx->d_lights = n_lights.release();
+    ctx->d_weights = n_weights.release();
+    ctx->d_cdf = n_cdf.release();
+    ctx->d_wall = n_wall.release();
+    ctx->d_spheres = n_spheres.release();
     ctx->geometry_kind = s->geometry_kind;
     ctx->n_lights = nl;
     ctx->n_spheres = s->n_spheres;
@@ -2320,29 +2360,29 @@ int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* himg) {
     if (!himg || !himg->pixels || !himg->counters) return fail(ctx, IPT_E_INVALID, "image pixels/counters are NULL");
     hipSetDevice(ctx->device);
     const size_t npix = (size_t)p->width * p->height;
-    ipt_image d{};
-    HIPCHECK(ctx, hipMalloc(&d.pixels, npix * 4));
-    HIPCHECK(ctx, hipMalloc(&d.counters, npix * 4));
-    if (himg->sums) HIPCHECK(ctx, hipMalloc(&d.sums, npix * 4));
-    if (himg->pixel_max) HIPCHECK(ctx, hipMalloc(&d.pixel_max, npix * 4));
+    DevBuf<float> pixels, sums, pmax;
+    DevBuf<uint32_t> counters;
+    HIPCHECK(ctx, hipMalloc(&pixels.p, npix * 4));
+    HIPCHECK(ctx, hipMalloc(&counters.p, npix * 4));
+    if (himg->sums) HIPCHECK(ctx, hipMalloc(&sums.p, npix * 4));
+    if (himg->pixel_max) HIPCHECK(ctx, hipMalloc(&pmax.p, npix * 4));
+    ipt_image d{pixels.p, counters.p, sums.p, pmax.p};
     hipStream_t st = ctx->stream;
     HIPCHECK(ctx, hipMemcpyAsync(d.pixels, himg->pixels, npix * 4, hipMemcpyHostToDevice, st));
     HIPCHECK(ctx, hipMemcpyAsync(d.counters, himg->counters, npix * 4, hipMemcpyHostToDevice, st));
     if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(d.sums, himg->sums, npix * 4, hipMemcpyHostToDevice, st));
     if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(d.pixel_max, himg->pixel_max, npix * 4, hipMemcpyHostToDevice, st));
     rc = render_chunks(ctx, p, &d, st, nullptr, nullptr);
-    if (rc == IPT_OK) {
-        HIPCHECK(ctx, hipMemcpyAsync(himg->pixels, d.pixels, npix * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(ctx, hipMemcpyAsync(himg->counters, d.counters, npix * 4, hipMemcpyDeviceToHost, st));
-        if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(himg->sums, d.sums, npix * 4, hipMemcpyDeviceToHost, st));
-        if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(himg->pixel_max, d.pixel_max, npix * 4, hipMemcpyDeviceToHost, st));
-        HIPCHECK(ctx, hipStreamSynchronize(st));
+    if (rc) {
+        (void)hipStreamSynchronize(st);  // no copy may still read the buffers when they are freed
+        return rc;
     }
-    hipFree(d.pixels);
-    hipFree(d.counters);
-    if (d.sums) hipFree(d.sums);
-    if (d.pixel_max) hipFree(d.pixel_max);
-    return rc;
+    HIPCHECK(ctx, hipMemcpyAsync(himg->pixels, d.pixels, npix * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(ctx, hipMemcpyAsync(himg->counters, d.counters, npix * 4, hipMemcpyDeviceToHost, st));
+    if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(himg->sums, d.sums, npix * 4, hipMemcpyDeviceToHost, st));
+    if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(himg->pixel_max, d.pixel_max, npix * 4, hipMemcpyDeviceToHost, st));
+    HIPCHECK(ctx, hipStreamSynchronize(st));
+    return IPT_OK;
 }
 
 int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t* codes) {
@@ -2428,17 +2468,16 @@ int ipt_math_host(int fn, const float* in, float* out, int64_t n) {
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n) {
     if (!ctx || !in || !out || n < 0 || fn < 0 || fn > 15) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
-    float *din = nullptr, *dout = nullptr;
-    HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * 4));
-    HIPCHECK(ctx, hipMalloc(&dout, std::max<int64_t>(n, 1) * 4));
-    HIPCHECK(ctx, hipMemcpy(din, in, n * 4, hipMemcpyHostToDevice));
+    DevBuf<float> din, dout;
+    HIPCHECK(ctx, hipMalloc(&din.p, std::max<int64_t>(n, 1) * 4));
+    HIPCHECK(ctx, hipMalloc(&dout.p, std::max<int64_t>(n, 1) * 4));
+    HIPCHECK(ctx, hipMemcpy(din.p, in, n * 4, hipMemcpyHostToDevice));
     const long long blocks = (n + 255) / 256;
-    if (blocks > 0) hipLaunchKernelGGL(math_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, fn, din, dout, (long long)n);
+    if (blocks > 0)
+        hipLaunchKernelGGL(math_kernel, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, fn, din.p, dout.p, (long long)n);
     HIPCHECK(ctx, hipGetLastError());
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-    HIPCHECK(ctx, hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost));
-    hipFree(din);
-    hipFree(dout);
+    HIPCHECK(ctx, hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
     return IPT_OK;
 }
 
@@ -2462,24 +2501,21 @@ static int ddf_call(ipt_ctx* ctx, int value_mode, int kind, const float* params,
         return fail(ctx, IPT_E_INVALID, "ipt_ddf: light index out of range");
     hipSetDevice(ctx->device);
     const size_t in_w = 3, out_w = value_mode ? 1 : 3;
-    float *dp = nullptr, *din = nullptr, *dout = nullptr;
-    HIPCHECK(ctx, hipMalloc(&dp, 8 * sizeof(float)));
-    HIPCHECK(ctx, hipMalloc(&din, std::max<int64_t>(n, 1) * in_w * sizeof(float)));
-    HIPCHECK(ctx, hipMalloc(&dout, std::max<int64_t>(n, 1) * out_w * sizeof(float)));
+    DevBuf<float> dp, din, dout;
+    HIPCHECK(ctx, hipMalloc(&dp.p, 8 * sizeof(float)));
+    HIPCHECK(ctx, hipMalloc(&din.p, std::max<int64_t>(n, 1) * in_w * sizeof(float)));
+    HIPCHECK(ctx, hipMalloc(&dout.p, std::max<int64_t>(n, 1) * out_w * sizeof(float)));
     float hp[8] = {0};
     for (int k = 0; k < (kind == 0 || kind == 3 ? 3 : (kind == 1 ? 4 : 6)); ++k) hp[k] = params[k];
-    HIPCHECK(ctx, hipMemcpy(dp, hp, sizeof hp, hipMemcpyHostToDevice));
-    HIPCHECK(ctx, hipMemcpy(din, in, n * in_w * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(dp.p, hp, sizeof hp, hipMemcpyHostToDevice));
+    HIPCHECK(ctx, hipMemcpy(din.p, in, n * in_w * sizeof(float), hipMemcpyHostToDevice));
     if (n > 0)
         hipLaunchKernelGGL(ddf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, value_mode, kind,
-                           dp, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->n_lights, din, (long long)n, dout,
+                           dp.p, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->n_lights, din.p, (long long)n, dout.p,
                            ctx->d_cos_a, ctx->d_cos_b);
     HIPCHECK(ctx, hipGetLastError());
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-    HIPCHECK(ctx, hipMemcpy(out, dout, n * out_w * sizeof(float), hipMemcpyDeviceToHost));
-    hipFree(dp);
-    hipFree(din);
-    hipFree(dout);
+    HIPCHECK(ctx, hipMemcpy(out, dout.p, n * out_w * sizeof(float), hipMemcpyDeviceToHost));
     return IPT_OK;
 }
 
@@ -2501,24 +2537,22 @@ int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits,
         const int rc = ensure_frame_table(ctx, ctx->stream);
         if (rc) return rc;
     }
-    unsigned long long* d_bad = nullptr;
-    unsigned int* d_first = nullptr;
-    HIPCHECK(ctx, hipMalloc(&d_bad, sizeof(unsigned long long)));
-    HIPCHECK(ctx, hipMalloc(&d_first, sizeof(unsigned int)));
-    HIPCHECK(ctx, hipMemsetAsync(d_bad, 0, sizeof(unsigned long long), ctx->stream));
-    HIPCHECK(ctx, hipMemsetAsync(d_first, 0xff, sizeof(unsigned int), ctx->stream));
+    DevBuf<unsigned long long> d_bad;
+    DevBuf<unsigned int> d_first;
+    HIPCHECK(ctx, hipMalloc(&d_bad.p, sizeof(unsigned long long)));
+    HIPCHECK(ctx, hipMalloc(&d_first.p, sizeof(unsigned int)));
+    HIPCHECK(ctx, hipMemsetAsync(d_bad.p, 0, sizeof(unsigned long long), ctx->stream));
+    HIPCHECK(ctx, hipMemsetAsync(d_first.p, 0xff, sizeof(unsigned int), ctx->stream));
     const unsigned long long n = hi_bits - lo_bits;
     if (n > 0)
         hipLaunchKernelGGL(selfcheck_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, ctx->stream, fn,
-                           (unsigned long long)lo_bits, n, d_bad, d_first, ctx->d_frame_sc);
+                           (unsigned long long)lo_bits, n, d_bad.p, d_first.p, ctx->d_frame_sc);
     HIPCHECK(ctx, hipGetLastError());
     unsigned long long hb = 0;
     unsigned int hf = 0;
-    HIPCHECK(ctx, hipMemcpyAsync(&hb, d_bad, sizeof hb, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHECK(ctx, hipMemcpyAsync(&hf, d_first, sizeof hf, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipMemcpyAsync(&hb, d_bad.p, sizeof hb, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipMemcpyAsync(&hf, d_first.p, sizeof hf, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-    hipFree(d_bad);
-    hipFree(d_first);
     *mismatches = hb;
     *first_bad = hf;
     return IPT_OK;

@@ -97,13 +97,7 @@ __global__ __launch_bounds__(kPostBlock) void glare_kernel(const float* __restri
     if (live) out[(size_t)y * W + x] = v < 0.0f ? 0.0f : (v > cutoff ? cutoff : v);  // cimg::cut
 }
 
-template <class T>
-struct DevBuf {
-    T* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
+using ipt_internal::DevBuf;
 
 #define POSTCHECK(ctx, expr)                                                                             \
     do {                                                                                                 \

@@ -325,3 +325,27 @@ def test_sphere_grid_adversarial_bit_exact(gpu_ctx, oracle, k, r, cam_pos, cam_d
     ov, oc = ob.render_values(desc, p, 0)
     assert np.array_equal(gc, oc)
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+@pytest.mark.parametrize("fail_at", [1, 2, 7])
+def test_failed_upload_leaves_no_scene(gpu_ctx, oracle, monkeypatch, fail_at):
+    """ipt_upload_scene is transactional (ipt_capi.h): an allocation failure in
+    the second upload (injected at its k-th device allocation) returns an error
+    and leaves the context with no scene, so the next render fails with
+    IPT_E_NOSCENE instead of launching on freed or null scene buffers; a later
+    upload recovers and renders bit-exactly."""
+    desc = scenes.make_scene_spheres(400, seed=1)  # sphere grid + lights + spheres: 7 device buffers
+    p = capi.make_params(16, 12, 1, n_rays=8, depth_max=5)
+    gpu_ctx.upload_scene(scenes.make_scene_box())
+    gpu_ctx.render_values(p)
+    monkeypatch.setenv("IPT_TEST_FAIL_UPLOAD_ALLOC", str(fail_at))
+    with pytest.raises(capi.IptError) as e:
+        gpu_ctx.upload_scene(desc)
+    assert e.value.code == capi.IPT_E_OOM
+    monkeypatch.delenv("IPT_TEST_FAIL_UPLOAD_ALLOC")
+    with pytest.raises(capi.IptError) as e:
+        gpu_ctx.render_values(p)
+    assert e.value.code == capi.IPT_E_NOSCENE
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov))
