@@ -263,7 +263,10 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
       12 the 32-bit work-unit division over hashed (n, d) pairs (bit pattern),
       13 the range-free sqrtf on [2^-96, 2^126) (sqrtf elsewhere),
       14 / 15 sin / cos of the RotateDdf angle (float)acos((double)z) for
-         z = x; the self-check compares the path kernel's frame table */
+         z = x; the self-check compares the path kernel's frame table
+      16 (ipt_math_selfcheck only) the sphere-in-box frame without glm's
+         zero terms against the exact build, over directions hashed from
+         the bit pattern (incl. zero / tiny x and y) */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
 /* Device self-check of the fast math paths: for every float bit pattern b in

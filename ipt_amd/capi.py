@@ -328,6 +328,7 @@ MATH_FNS = {"acosf": 0, "sinf": 1, "cosf": 2, "acos_f64_f32": 3, "sincosf_sin": 
             "sincosf_cos": 5, "sqrtf": 6, "div_pi": 7, "two_pi_times": 8, "div_pairs": 9,
             "div_inrange_pairs": 10, "longer_pairs": 11, "udiv_exact_pairs": 12,
             "sqrt_inrange": 13, "frame_angle_sin": 14, "frame_angle_cos": 15}
+SELFCHECK_FRAME_FAST = 16  # ipt_math_selfcheck only: fast vs exact sphere-in-box frame
 
 
 def shard_plan(p: Params):

@@ -195,8 +195,14 @@ struct KParams {
     const float* __restrict__ cos_a;      // [2^24] CosineDdf table by u1's 24 bits: sin(acos(sqrt(u1)))
     const float2* __restrict__ cos_b;     // [2^24] by u2's 24 bits: (cos phi, sin phi)
     const float2* __restrict__ frame_sc;  // frame_table_kernel: RotateDdf angle (sin, cos) by to.z
+    const uint4* __restrict__ rg;         // IPT_RAYGEN: [total_units][2] raygen_kernel records
+    int count;                            // raygen_kernel: accumulate the drift counter
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
+
+#ifndef IPT_RAYGEN
+#define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
+#endif
 
 // floor(n / d) for 32-bit n, d >= 1 from a double reciprocal: the estimate's
 // error is below (n/d) * 2^-51 < 1/d (n < 2^32), i.e. below the distance of a
@@ -243,6 +249,9 @@ constexpr uint32_t kFrameTabSpan = 0x04000000u;  // bits(1.0) - bits(2^-8)
 constexpr size_t kFrameTabEntries = 2 * ((size_t)kFrameTabSpan + 1);
 #ifndef IPT_FRAME_TAB
 #define IPT_FRAME_TAB 1  // +8.6 % C2
+#endif
+#ifndef IPT_FRAME_FAST
+#define IPT_FRAME_FAST 1  // sphere-in-box frames without glm's zero terms (make_frame_sc_fast)
 #endif
 __device__ __forceinline__ void frame_sc_lookup(const float2* __restrict__ tab, vec3 to, float& s, float& c) {
     const uint32_t u = f2u(to.z), m = u & 0x7fffffffu;
@@ -612,6 +621,83 @@ __host__ __device__ constexpr bool resumable_lights(int lmode, int geom) {
 __host__ __device__ constexpr int waves_per_simd(int geom, int lmode) {
     return (resumable_geom(geom) || resumable_lights(lmode, geom)) ? IPT_RES_WAVES : IPT_WAVES_PER_SIMD;
 }
+// render_sample's per-sample work before ray_power (main.cpp:192-211) for
+// work unit `unit` (pass-major, then candidate row, then column): the absolute
+// pass and source pixel (the Philox counter), the two jitter draws, the
+// GridRenderPlane drift code (and the flags of drifted samples), the camera
+// ray. A unit whose sample lands outside the image or in another shard's row
+// gets its value (0) and code stored here and is not traced.
+struct RayGen {
+    vec3 rd;
+    uint32_t a0, a1, a2, a3, rpass, rpix;
+    bool valid, drift;
+};
+__device__ __forceinline__ RayGen new_path_setup(const KParams& kp, unsigned long long unit, bool sharded,
+                                                 const int* cand_rows) {
+    RayGen g;
+#if IPT_UDIV32
+    const uint32_t u32 = (uint32_t)unit;
+    const uint32_t s = udiv_exact(u32, kp.per_pass32, kp.inv_per_pass);
+    const uint32_t rem = u32 - s * kp.per_pass32;
+    const int cand = (int)udiv_exact(rem, (uint32_t)kp.W, kp.inv_w);
+    const int ix = (int)(rem - (uint32_t)cand * (uint32_t)kp.W);
+#else
+    const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
+    const unsigned long long s = unit / per_pass;
+    const unsigned long long rem = unit - s * per_pass;
+    const int cand = (int)(rem / (unsigned long long)kp.W);
+    const int ix = (int)(rem - (unsigned long long)cand * kp.W);
+#endif
+    const int iy = sharded ? cand_rows[cand] : cand;
+    g.rpass = (uint32_t)(kp.spp_offset + (int)s);
+    g.rpix = (uint32_t)(iy * kp.W + ix);
+    philox_fill(g.a0, g.a1, g.a2, g.a3, 0u, g.rpass, g.rpix, kp.key0, kp.key1);
+    const float x = jitter_coord(ix, u01(g.a0), kp.W);
+    const float y = jitter_coord(iy, u01(g.a1), kp.H);
+    int xi, yi;
+    grid_index(x, y, kp.W, kp.H, &xi, &yi);
+    const int yn = nominal_row(iy, kp.H);
+    const int dx = xi - ix, dy = yi - yn;
+    uint8_t code = 0xff;
+    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < kp.W && yi < kp.H)
+        code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
+    g.drift = code != 0x05 && code != 0xff;
+    if (g.drift) {
+        kp.flags[(size_t)yn * kp.W + ix] = 1;
+        kp.flags[(size_t)yi * kp.W + xi] = 1;
+    }
+    g.valid = !(code == 0xff || !owned_row(kp, yi));
+    g.rd = v3(0, 0, 0);
+    if (!g.valid) {
+        // not ours (halo row of another shard) or out of range
+        kp.values[unit] = 0.0f;
+        kp.codes[unit] = code == 0xff ? code : (uint8_t)0xfe;
+    } else {
+        kp.codes[unit] = code;
+        g.rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
+    }
+    return g;
+}
+
+// One thread per work unit of the launch: new_path_setup at full lane
+// utilisation (inside the persistent path kernel a refill serves ~2 lanes of a
+// wave), written as two 16-byte records {rd.xyz, valid} {a2, a3, pass, pixel}
+// that the path kernel's refill reads.
+__global__ __launch_bounds__(256) void raygen_kernel(const KParams kp) {
+    const unsigned long long unit = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (unit >= kp.total_units) return;
+    const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
+    const RayGen g = new_path_setup(kp, unit, sharded, kp.cand_rows);
+    uint4* out = const_cast<uint4*>(kp.rg) + 2 * unit;
+    out[0] = make_uint4(__float_as_uint(g.rd.x), __float_as_uint(g.rd.y), __float_as_uint(g.rd.z), g.valid ? 1u : 0u);
+    out[1] = make_uint4(g.a2, g.a3, g.rpass, g.rpix);
+    if (kp.count) {
+        const uint64_t m = __ballot(g.drift);
+        if (m && (threadIdx.x & 63) == (unsigned)(__ffsll((long long)m) - 1))
+            atomicAdd(&kp.counters[10], (unsigned long long)__popcll(m));
+    }
+}
+
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
     extern __shared__ float lds[];
@@ -944,7 +1030,16 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     const vec3 to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
                     float fs = 0.0f, fc = 0.0f;
                     frame_sc_lookup(kp.frame_sc, to, fs, fc);
-                    f = make_frame_sc<kFrameInrange>(to, fs, fc);
+                    if (kFrameInrange && IPT_FRAME_FAST) {
+                        // without the zero terms; the rare lanes where a term
+                        // could decide a zero's sign take the exact build
+                        bool ok;
+                        f = make_frame_sc_fast(to, fs, fc, ok);
+                        if (__builtin_expect(__any(!ok), 0))
+                            if (!ok) f = make_frame_sc<kFrameInrange>(to, fs, fc);
+                    } else {
+                        f = make_frame_sc<kFrameInrange>(to, fs, fc);
+                    }
                 } else if (kFrameInrange)
                     f = make_frame<true>(normalize_inrange_(nrm));
                 else
@@ -975,63 +1070,47 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         if (active && has_path && fresh) {
             IPT_PHASE(2);
             fresh = false;
-#if IPT_UDIV32
-            const uint32_t u32 = (uint32_t)unit;
-            const uint32_t s = udiv_exact(u32, kp.per_pass32, kp.inv_per_pass);
-            const uint32_t rem = u32 - s * kp.per_pass32;
-            const int cand = (int)udiv_exact(rem, (uint32_t)kp.W, kp.inv_w);
-            const int ix = (int)(rem - (uint32_t)cand * (uint32_t)kp.W);
-#else
-            const unsigned long long s = unit / per_pass;
-            const unsigned long long rem = unit - s * per_pass;
-            const int cand = (int)(rem / (unsigned long long)kp.W);
-            const int ix = (int)(rem - (unsigned long long)cand * kp.W);
-#endif
-            int iy = cand;
-            if (sharded) {
-                if (cand_in_lds)
-                    iy = cand_lds[cand];
-                else
-                    iy = kp.cand_rows[cand];
-            }
-            rpass = (uint32_t)(kp.spp_offset + (int)s);
-            rpix = (uint32_t)(iy * kp.W + ix);
-            philox_fill(w.a0, w.a1, w.a2, w.a3, 0u, rpass, rpix, kp.key0, kp.key1);
+            if (IPT_RAYGEN) {
+                // raygen_kernel ran render_sample's per-sample work for this
+                // unit (jitter, drift code and flags, camera ray, Philox block 0)
+                const uint4 r0 = kp.rg[2 * unit], r1 = kp.rg[2 * unit + 1];
+                if (r0.w == 0u) {
+                    has_path = false;  // not ours / out of range: already stored
+                } else {
+                    ro = kp.cam_pos;
+                    rd = v3(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z));
+                    w.a2 = r1.x;
+                    w.a3 = r1.y;
+                    rpass = r1.z;
+                    rpix = r1.w;
+                    blk = 0;
+                    need_b = true;  // block 1 is produced by the window refill of the next iteration
+                    k = 2;
+                    rdepth = 0;
+                    have_ray = true;
+                    if (COUNT) ++c_paths;
+                }
+            } else {
+            const RayGen g = new_path_setup(kp, unit, sharded, kp.cand_rows);
+            w.a0 = g.a0;
+            w.a1 = g.a1;
+            w.a2 = g.a2;
+            w.a3 = g.a3;
+            rpass = g.rpass;
+            rpix = g.rpix;
             blk = 0;
-            need_b = true;  // block 1 is produced by the window refill of the next iteration
+            need_b = true;
             k = 2;
-            const float x = jitter_coord(ix, u01(w.a0), kp.W);
-            const float y = jitter_coord(iy, u01(w.a1), kp.H);
-            int xi, yi;
-            grid_index(x, y, kp.W, kp.H, &xi, &yi);
-            const int yn = nominal_row(iy, kp.H);
-            const int dx = xi - ix, dy = yi - yn;
-            uint8_t code = 0xff;
-            if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < kp.W && yi < kp.H)
-                code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
-            if (code != 0x05 && code != 0xff) {
-                kp.flags[(size_t)yn * kp.W + ix] = 1;
-                kp.flags[(size_t)yi * kp.W + xi] = 1;
-                if (COUNT) ++c_drift;
-            }
-            if (code == 0xff || !owned_row(kp, yi)) {
-                // not ours (halo row of another shard) or out of range
-                kp.values[unit] = 0.0f;
-                kp.codes[unit] = code == 0xff ? code : (uint8_t)0xfe;
+            if (COUNT && g.drift) ++c_drift;
+            if (!g.valid) {
                 has_path = false;
             } else {
-                kp.codes[unit] = code;
                 ro = kp.cam_pos;
-                rd = camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x, y);
-                if (IPT_ABL == 6) {
-                    uint32_t q0, q1, q2, q3;
-                    philox_fill(q0, q1, q2, q3, (uint32_t)kp.abl_zero, rpass, rpix, kp.key0, kp.key1);
-                    keep_alive(q0 ^ q1);
-                    keep_alive(camera_dir(kp.cam_right, kp.cam_up, kp.cam_dir, x + kp.abl_zero, y));
-                }
+                rd = g.rd;
                 rdepth = 0;
                 have_ray = true;
                 if (COUNT) ++c_paths;
+            }
             }
         }
 
@@ -1687,6 +1766,42 @@ __device__ float math_fn_exact(int fn, float x) {
     return math_fn(fn, x);
 }
 
+// Self-check 16: a sphere-in-box-like normal from the bit pattern b (hashed
+// coordinates with |nrm| around 0.5, plus the edge cases the fast frame must
+// hand to the exact build: zero or tiny x / y, both tiny, z = +-1 directions,
+// x = +-y) -> to = normalize(nrm); true when the fast frame says ok and any of
+// its 12 floats differs from make_frame_sc<true>'s bits.
+__device__ bool frame_fast_mismatch(uint32_t b) {
+    const uint32_t h1 = probe_hash(b), h2 = probe_hash(h1 ^ 0x9e3779b9u), h3 = probe_hash(h2 + 0x7f4a7c15u);
+    float x = (float)(int)(h1 >> 8) * 0x1p-24f - 0.5f;  // [-0.5, 0.5)
+    float y = (float)(int)(h2 >> 8) * 0x1p-24f - 0.5f;
+    float z = (float)(int)(h3 >> 8) * 0x1p-24f - 0.5f;
+    switch (b & 15u) {
+        case 0: x = 0.0f; break;
+        case 1: y = 0.0f; break;
+        case 2: x = u2f(h1 & 0x0fffffffu) * (h2 & 1 ? 1.0f : -1.0f); break;           // tiny x
+        case 3: x = u2f(h1 & 0x0fffffffu); y = -u2f(h2 & 0x0fffffffu); break;        // tiny x and y
+        case 4: x = -0.0f; y = u2f(h3 & 0x1fffffffu); break;
+        case 5: y = x; break;
+        case 6: y = -x; break;
+        case 7: x = u2f(h1 & 0x33ffffffu); y = u2f(h2 & 0x33ffffffu); break;         // |x|, |y| ~ 1e-7
+        default: break;
+    }
+    if (!(z != 0.0f)) z = 0.25f;
+    const vec3 to = normalize_inrange_(v3(x, y, z));
+    float s, c;
+    frame_angle_sc(to, &s, &c);
+    bool ok;
+    const Frame f = make_frame_sc_fast(to, s, c, ok);
+    if (!ok) return false;
+    const Frame e = make_frame_sc<true>(to, s, c);
+    const float* pf = &f.m0.x;
+    const float* pe = &e.m0.x;
+    bool diff = false;
+    for (int k = 0; k < 12; ++k) diff |= f2u(pf[k]) != f2u(pe[k]);
+    return diff;
+}
+
 __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long long n,
                                  unsigned long long* bad, unsigned int* first, const float2* __restrict__ ftab) {
     unsigned long long local = 0;
@@ -1694,6 +1809,13 @@ __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long lo
     for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t b = (uint32_t)(lo + i);
         const float x = u2f(b);
+        if (fn == 16) {  // make_frame_sc_fast == make_frame_sc<true> wherever it reports ok
+            if (frame_fast_mismatch(b)) {
+                ++local;
+                atomicMin(first, b);
+            }
+            continue;
+        }
         float a = math_fn(fn, x);
         const float e = math_fn_exact(fn, x);
         if (fn == 14 || fn == 15) {  // the path kernel's table lookup (frame_sc_lookup)
@@ -1749,6 +1871,7 @@ struct ipt_ctx {
     // work buffers
     float* d_values = nullptr;
     uint8_t* d_codes = nullptr;
+    uint4* d_rg = nullptr;  // raygen_kernel records, 2 x 16 B per element
     size_t work_cap = 0;  // elements
     uint8_t* d_flags = nullptr;
     size_t flags_cap = 0;
@@ -1823,15 +1946,20 @@ int ensure_work(ipt_ctx* ctx, size_t elems, size_t npix, int H, int n_cand) {
     if (elems > ctx->work_cap) {
         if (ctx->d_values) hipFree(ctx->d_values);
         if (ctx->d_codes) hipFree(ctx->d_codes);
+        if (ctx->d_rg) hipFree(ctx->d_rg);
         ctx->d_values = nullptr;
         ctx->d_codes = nullptr;
+        ctx->d_rg = nullptr;
         ctx->work_cap = 0;
         DevBuf<float> v;
         DevBuf<uint8_t> c;
+        DevBuf<uint4> g;
         HIPCHECK(ctx, hipMalloc(&v.p, elems * sizeof(float)));
         HIPCHECK(ctx, hipMalloc(&c.p, elems));
+        if (IPT_RAYGEN) HIPCHECK(ctx, hipMalloc(&g.p, elems * 2 * sizeof(uint4)));
         ctx->d_values = v.release();
         ctx->d_codes = c.release();
+        ctx->d_rg = g.release();
         ctx->work_cap = elems;
     }
     if (npix > ctx->flags_cap) {
@@ -1973,8 +2101,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     const int W = p->width, H = p->height;
     const size_t per_pass = (size_t)n_cand * W;
     if (per_pass == 0 || p->spp == 0) return IPT_OK;
-    // chunk passes so the radiance buffer stays <= 1 GiB of floats
-    const size_t budget = (size_t)1 << 28;
+    // chunk passes so that the work buffers stay bounded: 2^27 units = 512 MiB
+    // of radiance + 128 MiB of codes + 4 GiB of raygen records
+    const size_t budget = (size_t)1 << 27;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->spp, budget / per_pass));
     if (host_values) chunk = p->spp;  // debug path: one chunk
     int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
@@ -2054,9 +2183,15 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cos_b = ctx->d_cos_b;
         kp.frame_sc = ctx->d_frame_sc;
         kp.cand_lds = (p->n_shards > 1 && p->tile_rows > 0 && kp.n_cand <= kLdsCand) ? 1 : 0;
+        kp.rg = ctx->d_rg;
+        kp.count = count ? 1 : 0;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
+        if (IPT_RAYGEN) {
+            hipLaunchKernelGGL(raygen_kernel, dim3((unsigned)((kp.total_units + 255) / 256)), dim3(256), 0, st, kp);
+            HIPCHECK(ctx, hipGetLastError());
+        }
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));  // path kernel alone (raygen is in the call's time)
         if (susp <= 4)
             rc = launch_path<4>(ctx, kp, st, count);
         else if (susp <= 8)
@@ -2160,7 +2295,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
-                    ctx->d_values, ctx->d_codes, ctx->d_flags, ctx->d_cand_rows,
+                    ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
                     ctx->d_grid_start, ctx->d_grid_items, ctx->d_frame_sc};
     for (void* b : bufs)
@@ -2529,7 +2664,7 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
                        uint32_t* first_bad) {
-    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 15 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 16 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
         return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     if (fn == 14 || fn == 15) {

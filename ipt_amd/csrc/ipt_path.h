@@ -101,6 +101,42 @@ IPT_HD Frame make_frame_sc(vec3 to, float s, float c) {
     f.iz = v3(I.c[0].z, I.c[1].z, I.c[2].z);
     return f;
 }
+// make_frame_sc<true> without its zero terms. glm's cross((0,0,1), to) has
+// z = 0*to.y - to.x*0, so ax.z and temp.z are signed zeros; glm::rotate's
+// product with the identity adds 0*R terms to every entry. For finite x,
+// x + (+-0) == x and (+-0) - x == -x whenever x != 0, so when all nine
+// rotation entries R are non-zero (and `to` is finite) every dropped term only
+// met a non-zero partner and the frame is bit-identical to make_frame_sc<true>.
+// `ok` reports that condition; the caller takes the exact path otherwise
+// (axis replaced by (1,0,0), to.x or to.y zero, an underflowed product).
+IPT_HD Frame make_frame_sc_fast(vec3 to, float s, float c, bool& ok) {
+    const float axx = -to.y, axy = to.x;  // cross((0,0,1), to).xy when non-zero
+    const float q = axx * axx + axy * axy;
+    const float r = sqrt_inrange_(q);
+    const float inv = div_inrange_(1.0f, r);
+    const float ax = axx * inv, ay = axy * inv;
+    const float omc = 1.0f - c;
+    const float tx = omc * ax, ty = omc * ay;
+    const float r00 = c + tx * ax, r01 = tx * ay, r02 = -(s * ay);
+    const float r10 = ty * ax, r11 = c + ty * ay, r12 = s * ax;
+    const float r20 = s * ay, r21 = -(s * ax), r22 = c;
+    // q >= 2^-80 and r >= 1e-6: the exact path's axis is not replaced; q
+    // finite: `to` is finite (a NaN/inf component reaches q)
+    const float mn = fminf(fminf(fminf(fabs_(r00), fabs_(r01)), fminf(fabs_(r02), fabs_(r10))),
+                           fminf(fminf(fabs_(r11), fabs_(r12)), fminf(fabs_(r21), fabs_(r22))));
+    ok = (mn > 0.0f) & (q >= 0x1p-80f) & (q < inf_()) & !lt_1em6(r);
+    mat3 M;
+    M.c[0] = v3(r00, r01, r02);
+    M.c[1] = v3(r10, r11, r12);
+    M.c[2] = v3(r20, r21, r22);
+    const mat3 I = inverse<true>(M);
+    Frame f;
+    f.m0 = M.c[0];
+    f.m1 = M.c[1];
+    f.m2 = M.c[2];
+    f.iz = v3(I.c[0].z, I.c[1].z, I.c[2].z);
+    return f;
+}
 template <bool INRANGE = false>
 IPT_HD Frame make_frame(vec3 to) {
     float s, c;

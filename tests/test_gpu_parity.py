@@ -130,6 +130,16 @@ def test_fast_math_exhaustive(gpu_ctx, fn):
     assert bad == 0, (fn, bad, hex(first))
 
 
+def test_fast_frame_matches_exact(gpu_ctx):
+    """The sphere-in-box frame without glm's zero terms (make_frame_sc_fast)
+    equals the exact RotateDdf build (make_frame_sc<true>) bit for bit on every
+    direction where it reports ok: 2^32 directions hashed from the bit
+    pattern, a quarter of them edge cases (zero, -0, tiny or ~1e-7 x and y,
+    x = +-y) that must either match or be handed to the exact build."""
+    bad, first = gpu_ctx.math_selfcheck(capi.SELFCHECK_FRAME_FAST)
+    assert bad == 0, (bad, hex(first))
+
+
 @pytest.mark.parametrize("n_shards", [2, 3])
 def test_sharded_render_matches_whole_frame(gpu_ctx, oracle, n_shards):
     """Tile-sharded rendering (one shard per call, as one rank per GPU does)
