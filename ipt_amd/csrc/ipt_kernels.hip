@@ -200,6 +200,16 @@ struct KParams {
     float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
 
+#ifndef IPT_SETUP_WAIT
+#define IPT_SETUP_WAIT 1  // drain the setup loads before the step loop
+#endif
+#ifndef IPT_PF
+#define IPT_PF 0  // the iteration prologue one step ahead (measured -1 to -2 %: instruction cost)
+#endif
+#ifndef IPT_FRAME_PF
+#define IPT_FRAME_PF 3  // the next step's frame-table entry gathered a step ahead: 1 at the
+                        // step's end, 2 right after the geometry trace (before resolve)
+#endif
 #ifndef IPT_RAYGEN
 #define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
 #endif
@@ -257,7 +267,12 @@ __device__ __forceinline__ void frame_sc_lookup(const float2* __restrict__ tab, 
     const uint32_t u = f2u(to.z), m = u & 0x7fffffffu;
     const bool in = m - kFrameTabLo <= kFrameTabSpan;
     if (in) {
+#ifdef IPT_EXP_FRAME_MASK
+        // timing experiment only (quantised angle): few cache lines touched
+        const float2 e = tab[(((m - kFrameTabLo) << 1) | (u >> 31)) & IPT_EXP_FRAME_MASK];
+#else
         const float2 e = tab[((m - kFrameTabLo) << 1) | (u >> 31)];
+#endif
         s = e.x;
         c = e.y;
     }
@@ -778,6 +793,11 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     const bool n_pow2 = kp.n_rays > 0 && (kp.n_rays & (kp.n_rays - 1)) == 0;
     const int n_log2 = n_pow2 ? 31 - __clz(kp.n_rays) : 0;
 
+    // the setup's vector loads (the single light, weights) complete here, so
+    // the step loop's waits never drain them (a conservative vmcnt(0) inside
+    // the loop would also drain the step's young table gathers)
+    if (IPT_SETUP_WAIT) __builtin_amdgcn_s_waitcnt(0);
+
     // wave-local unit pool (uniform)
     unsigned long long pool_next = 0, pool_end = 0;
 
@@ -786,6 +806,17 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     // never stored: walls load theirs from the LDS table, sphere nodes rebuild
     // theirs (make_frame) in the frame phase of the step after a push or pop.
     bool active = true, has_path = false, fresh = false, need_frame = false, need_b = false;
+    // the next iteration's pick and draws (IPT_PF: prepared one step ahead)
+    int pick = -1;
+    float u1 = 0.0f, u2 = 0.0f, tr = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
+    bool pf = false;  // pick/u1/u2/cs_* hold the lane's next iteration
+    // IPT_FRAME_PF: the frame-table entry (sin, cos) of the node the lane will
+    // build a frame for in the next step, gathered at the end of this step;
+    // pfz = the to.z bits it belongs to (checked at use)
+    float pfs = 0.0f, pfc = 0.0f;
+    uint32_t pfz = 0xffffffffu;
+    vec3 pto = v3(0, 0, 0);  // IPT_FRAME_PF == 3: the prepared frame's `to`
+    bool pfok = false;
     unsigned long long unit = 0;
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
@@ -859,6 +890,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         IPT_STAMP_AT(1);  // refill
         if (active) { IPT_PHASE(0); }
         // ------------------------------- phase 1: finalize + pop (main.cpp:177-183)
+        // (IPT_FRAME_PF == 3: at the end of the previous step instead -- the
+        // same operations on the same state, nothing changes it in between but
+        // the refill of lanes without a path)
+        auto pop_node = [&]() {
         if (IPT_POPMASK && active && has_path && !fresh && !((kRes || kResL) && tracing) &&
             ti >= (kp.n_rays >> tdepth)) {
             // the node is done: unwind every suspended level whose node has run
@@ -922,6 +957,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 need_frame = tkind >= 5 && fdepth != lvl;
             }
         }
+        };
+        if (IPT_FRAME_PF != 3) pop_node();
 
         IPT_STAMP_AT(2);  // finalize + pop
         // the current node's frame normal (frame build below)
@@ -941,12 +978,44 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         constexpr bool kFrameInrange = IPT_FRAME_INRANGE && GEOM == IPT_GEOM_SPHERE_IN_BOX;
         const bool fneed = need_frame && has_path && !fresh && !((kRes || kResL) && tracing);
         IPT_STAMP_AT(3);  // (new path: later in the step)
-        // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153)
+        // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153) and,
+        // for a cosine pick, the CosineDdf table gathers. IPT_PF: run for the
+        // NEXT iteration right after this step's direction phase (the draws are
+        // sequential per path whichever node iterates next), so the gathers have
+        // the rest of the step to land instead of being drained by the frame
+        // pass's wait; the lane carries pick/u1/u2/cs_* to its next iteration.
         const bool iter_lane = active && has_path && !fresh && !((kRes || kResL) && tracing);
-        int pick = -1;
-        float u1 = 0.0f, u2 = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
-        if (iter_lane) {
-            IPT_PHASE(3);
+        // the cosine pick's table indices; the gathers are issued by the whole
+        // wave after the prologue (index 0 for the other lanes) so that the
+        // number of loads between a gather and its wait is the same on every
+        // path and the compiler's waits drain only what they wait for
+        uint32_t gi_a = 0, gi_b = 0;
+        bool gcos = false;
+        // (`ran`: the lane ran the prologue in this step. In the resumable
+        // instances a lane keeps its prepared iteration while its walk goes on,
+        // so there the gathers stay per lane.)
+        auto gathers = [&](bool ran) {
+#ifdef IPT_EXP_GATHER_MASK
+            // timing experiment only (quantised samples): the draws' low bits
+            // dropped, so the table reads touch few cache lines
+            gi_a &= IPT_EXP_GATHER_MASK;
+            gi_b &= IPT_EXP_GATHER_MASK;
+#endif
+            if constexpr (kRes || kResL) {
+                if (ran && gcos) {
+                    tr = kp.cos_a[gi_a];
+                    const float2 tb = kp.cos_b[gi_b];
+                    cs_c = tb.x;
+                    cs_s = tb.y;
+                }
+            } else {
+                tr = kp.cos_a[gcos ? gi_a : 0u];
+                const float2 tb = kp.cos_b[gcos ? gi_b : 0u];
+                cs_c = tb.x;
+                cs_s = tb.y;
+            }
+        };
+        auto prologue = [&]() {
             if ((k >> 2) != blk) {
                 w.a0 = w.b0; w.a1 = w.b1; w.a2 = w.b2; w.a3 = w.b3;
                 ++blk;
@@ -985,20 +1054,24 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 u2 = u01(r2);
                 if (c == nl) {
                     // CosineDdf::sample (ddf.cpp:223-231) of (u1, u2): (cos_alpha, r) x
-                    // (cos phi, sin phi) looked up by the draws' 24 bits; consumed after
-                    // barrier B, so the loads' latency hides behind the frame pass
+                    // (cos phi, sin phi) looked up by the draws' 24 bits
                     // (a non-temporal hint measured slower on C2 and C5)
                     // (cos_alpha = sqrtf(u1) is recomputed in the direction phase)
-                    const float tr = kp.cos_a[r1 >> 8];
-                    const float2 tb = kp.cos_b[r2 >> 8];
-                    u2 = tr;
-                    cs_c = tb.x;
-                    cs_s = tb.y;
+                    gi_a = r1 >> 8;
+                    gi_b = r2 >> 8;
+                    gcos = true;
                 }
                 k += 3;
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
             }
+        };
+        if (!IPT_PF) {
+            if (iter_lane) {
+                IPT_PHASE(3);
+                prologue();
+            }
+            gathers(iter_lane);
         }
         // (the frame build sits between the table gathers' issue and their use)
         // ------------- phase 3: the current node's RotateDdf frame when it is a sphere node without one
@@ -1027,9 +1100,38 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (IPT_FRAME_TAB && GEOM == IPT_GEOM_SPHERE_IN_BOX) {
                     // (sphere-list scenes: measured slower with the table's
                     // gathers in their latency-bound walks)
-                    const vec3 to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                    vec3 to;
                     float fs = 0.0f, fc = 0.0f;
-                    frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                    if (IPT_FRAME_PF == 3) {
+                        // `to` and its frame-table entry, prepared at the end of
+                        // the previous step (pfok: `to` inside the table's range)
+                        to = pto;
+                        fs = pfs;
+                        fc = pfc;
+                        if (__builtin_expect(__any(!pfok), 0))
+                            if (!pfok) {
+                                to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                                frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                                keep_alive(fs);  // its wait stays in this rare branch
+                                keep_alive(fc);
+                            }
+                        pfok = false;
+                    } else if (IPT_FRAME_PF) {
+                        to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                        // normally gathered at the end of the previous step
+                        const bool have = f2u(to.z) == pfz;
+                        fs = pfs;
+                        fc = pfc;
+                        if (__builtin_expect(__any(!have), 0))
+                            if (!have) {
+                                frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                                keep_alive(fs);  // its wait stays in this rare branch
+                                keep_alive(fc);
+                            }
+                    } else {
+                        to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                        frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                    }
                     if (kFrameInrange && IPT_FRAME_FAST) {
                         // without the zero terms; the rare lanes where a term
                         // could decide a zero's sign take the exact build
@@ -1073,7 +1175,11 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             if (IPT_RAYGEN) {
                 // raygen_kernel ran render_sample's per-sample work for this
                 // unit (jitter, drift code and flags, camera ray, Philox block 0)
-                const uint4 r0 = kp.rg[2 * unit], r1 = kp.rg[2 * unit + 1];
+                // both records load together and are consumed here: no load of
+                // this (divergent) phase is left in flight for later waits
+                uint4 r0 = kp.rg[2 * unit], r1 = kp.rg[2 * unit + 1];
+                keep_alive(r0);
+                keep_alive(r1);
                 if (r0.w == 0u) {
                     has_path = false;  // not ours / out of range: already stored
                 } else {
@@ -1086,6 +1192,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     blk = 0;
                     need_b = true;  // block 1 is produced by the window refill of the next iteration
                     k = 2;
+                    pf = false;
                     rdepth = 0;
                     have_ray = true;
                     if (COUNT) ++c_paths;
@@ -1101,6 +1208,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             blk = 0;
             need_b = true;
             k = 2;
+            pf = false;
             if (COUNT && g.drift) ++c_drift;
             if (!g.valid) {
                 has_path = false;
@@ -1115,9 +1223,26 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }
 
         // ------------------------- phase 3b: the iteration's direction (main.cpp:149-163)
+        // kLightsOne: both candidate directions are computed by every lane and
+        // one is selected (a mixed wave runs both anyway), so the CosineDdf
+        // gathers have an unconditional consumer and stay unconditional loads
+        vec3 dir_bf = v3(0, 0, 0);
+        if constexpr (LMODE == kLightsOne) {
+            Frame fm;
+            fm.m0 = v3(frc[0 * kFrameStride], frc[1 * kFrameStride], frc[2 * kFrameStride]);
+            fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
+            fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
+            const vec3 cdir = frame_apply(fm, v3(tr * cs_c, tr * cs_s, sqrt_inrange_(u1)));
+            const vec3 ldir = light_sample_dir<false>(LS.one, tpos, u1, u2);
+            const vec3 zero = v3(0, 0, 0);
+            dir_bf = pick < nl ? ldir : (pick == nl ? cdir : zero);
+        }
         if (iter_lane) {
             vec3 dir = v3(0, 0, 0);
-            if (pick < nl) {
+            if (LMODE == kLightsOne) {
+                dir = dir_bf;
+                if (COUNT && pick < nl) ++c_lsamp;
+            } else if (pick < nl) {
                 IPT_PHASE(7);
                 dir = light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1, u2);
                 if (IPT_ABL == 7)
@@ -1132,7 +1257,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // with u2 = r and cos_alpha = sqrtf(u1)
                 // u1 is 0 or in [2^-24, 1): the range-free root is sqrtf there
                 // (math probe 13 is exhaustive on [2^-96, 2^126); sqrt_inrange_(0) = +0)
-                dir = frame_apply(fm, v3(u2 * cs_c, u2 * cs_s, sqrt_inrange_(u1)));
+                dir = frame_apply(fm, v3(tr * cs_c, tr * cs_s, sqrt_inrange_(u1)));
             }
             ++ti;
             if (COUNT) ++c_iter;
@@ -1145,6 +1270,17 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 have_ray = true;
                 is_iter = true;
             }
+            pf = false;
+        }
+        if (IPT_PF) {
+            const bool ran = active && has_path && !pf;
+            if (ran) {
+                // the next iteration of this path (incl. a new path's first)
+                IPT_PHASE(3);
+                prologue();
+                pf = true;
+            }
+            gathers(ran);
         }
         IPT_STAMP_AT(8);  // direction
         // --------------------------------------------- phase 4: trace + resolve
@@ -1330,6 +1466,13 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
             }
         } else {
+        // IPT_FRAME_PF == 2: the trace's results wait for resolve until the next
+        // node's frame-table gather has been issued (see below)
+        constexpr bool kFramePf2 = IPT_FRAME_PF == 2 && IPT_FRAME_TAB && kFrameInrange && !kRes;
+        bool rs_do = false, rs_has_li = false;
+        float rs_t = inf_(), rs_mult = 0.0f, rs_li_pow = 0.0f;
+        int rs_prim = -1;
+        vec3 rs_li_pos = v3(0, 0, 0);
         if (have_ray) {
             IPT_PHASE(8);
             // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
@@ -1449,8 +1592,71 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     }
                     IPT_STAMP_AT(10);  // mixture value + geometry trace
                 }
-                resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
+                if (kFramePf2) {
+                    rs_do = true;
+                    rs_t = t;
+                    rs_prim = prim;
+                    rs_mult = mult;
+                    rs_has_li = has_li;
+                    rs_li_pos = li_pos;
+                    rs_li_pow = li_pow;
+                } else {
+                    resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
+                }
             }
+        }
+        if constexpr (kFramePf2) {
+            // the node current at the next step and whether its frame is built
+            // then -- a sphere node this ray pushes (resolve's decision, computed
+            // the same way), or the pop target (the first unfinished ancestor, as
+            // the pop computes it) when the node has run all its iterations and a
+            // descendant overwrote that node's column -- and its frame-table
+            // gather, issued now so that resolve, the pop and the next step's
+            // prologue cover its latency (the frame build's only memory access)
+            bool want = false, push = false;
+            vec3 ppos = v3(0, 0, 0);
+            if (active && has_path) {
+                if (rs_do) {
+                    const bool has_si = rs_prim >= 0;
+                    const vec3 si_pos = ro + rd * rs_t;
+                    const vec3 ea = si_pos - ro, eb = rs_li_pos - ro;
+                    const bool lg = (rs_has_li && has_si) ? longer_sq(dot(ea, ea), dot(eb, eb)) : false;
+                    const bool li_wins = rs_has_li && (!has_si || lg);
+                    push = rdepth < kp.depth_max && !li_wins && has_si && (kp.n_rays >> rdepth) != 0;
+                    if (push && rs_prim >= 5) {
+                        want = true;
+                        ppos = si_pos;
+                    }
+                }
+                if (!push && (is_iter || !rs_do) && ti >= (kp.n_rays >> tdepth)) {
+                    const uint32_t m = ~finm & ((1u << tdepth) - 1u);
+                    const int stop = m ? 31 - (int)__clz(m) : -1;
+                    if (stop >= 0 && fdepth != stop) {
+                        const float* b = stk + (size_t)stop * kStackFields * kBlock + tid;
+                        if ((__float_as_int(b[5 * kBlock]) >> 8) >= 5) {
+                            want = true;
+                            ppos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
+                        }
+                    }
+                }
+            }
+            uint32_t idx = 0, u = 0xffffffffu;
+            if (want) {
+                const vec3 to = normalize_inrange_(ppos);
+                u = f2u(to.z);
+                const uint32_t mz = u & 0x7fffffffu;
+                if (mz - kFrameTabLo <= kFrameTabSpan) idx = ((mz - kFrameTabLo) << 1) | (u >> 31);
+                else u = 0xffffffffu;
+            }
+            // issued by the whole wave (index 0 for the other lanes, whose pfz
+            // marks the entry unused) and consumed in the next step's frame pass
+            const float2 e = kp.frame_sc[idx];
+            pfs = e.x;
+            pfc = e.y;
+            pfz = u;
+            if (rs_do)
+                resolve(rdepth < kp.depth_max, rs_t, rs_prim, ro, rd, rdepth, is_iter, rs_mult, rs_has_li, rs_li_pos,
+                        rs_li_pow);
         }
         if (kRes && tracing) {
             IPT_PHASE(9);
@@ -1469,6 +1675,65 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             }
         }
         }  // !kResL
+        if constexpr (IPT_FRAME_PF == 3) {
+            pop_node();
+            if constexpr (IPT_FRAME_TAB && kFrameInrange) {
+                // the frame the lane builds in the next step (a sphere node
+                // pushed in this step, or popped back to with its column
+                // overwritten): `to` and the table gather now, consumed there
+                if (need_frame && active && has_path) {
+                    const vec3 to = normalize_inrange_(tpos);
+                    const uint32_t u = f2u(to.z), mz = u & 0x7fffffffu;
+                    pfok = mz - kFrameTabLo <= kFrameTabSpan;
+                    if (pfok) {
+                        const float2 e = kp.frame_sc[((mz - kFrameTabLo) << 1) | (u >> 31)];
+                        pfs = e.x;
+                        pfc = e.y;
+                        pto = to;
+                    }
+                }
+            }
+        }
+        if constexpr (IPT_FRAME_PF == 1 && IPT_FRAME_TAB && kFrameInrange) {
+            // the node current at the next step and whether its frame is built
+            // then: a sphere node pushed this step, or the pop target (the first
+            // unfinished ancestor, as the pop computes it) when this node has run
+            // all its iterations and a descendant overwrote that node's column.
+            // Its frame-table entry is gathered now, a step before the frame
+            // pass needs it (the gather is the frame build's only memory access).
+            bool want = false;
+            vec3 ppos = tpos;
+            if (active && has_path && !fresh) {
+                if (need_frame) {
+                    want = true;
+                } else if (ti >= (kp.n_rays >> tdepth)) {
+                    const uint32_t m = ~finm & ((1u << tdepth) - 1u);
+                    const int stop = m ? 31 - (int)__clz(m) : -1;
+                    if (stop >= 0 && fdepth != stop) {
+                        const float* b = stk + (size_t)stop * kStackFields * kBlock + tid;
+                        const int kind = __float_as_int(b[5 * kBlock]) >> 8;
+                        if (kind >= 5) {
+                            want = true;
+                            ppos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
+                        }
+                    }
+                }
+            }
+            uint32_t idx = 0, u = 0xffffffffu;
+            if (want) {
+                const vec3 to = normalize_inrange_(ppos);
+                u = f2u(to.z);
+                const uint32_t mz = u & 0x7fffffffu;
+                if (mz - kFrameTabLo <= kFrameTabSpan) idx = ((mz - kFrameTabLo) << 1) | (u >> 31);
+                else u = 0xffffffffu;
+            }
+            // issued by the whole wave (index 0 for the other lanes, whose pfz
+            // marks the entry unused) and consumed in the next step's frame pass
+            const float2 e = kp.frame_sc[idx];
+            pfs = e.x;
+            pfc = e.y;
+            pfz = u;
+        }
     }
 
     if (IPT_STAMP && lane == 0)
