@@ -210,6 +210,18 @@ struct KParams {
 #define IPT_FRAME_PF 3  // the next step's frame-table entry gathered a step ahead: 1 at the
                         // step's end, 2 right after the geometry trace (before resolve)
 #endif
+#ifndef IPT_COSB_INLINE
+#define IPT_COSB_INLINE 1  // (cos phi, sin phi) of CosineDdf computed instead of gathered (+11 % C2)
+#endif
+#ifndef IPT_COSA_INLINE
+#define IPT_COSA_INLINE 0  // with IPT_COSB_INLINE: CosineDdf's r = sin(acos(sqrt(u1))) computed too
+#endif
+#ifndef IPT_FRAME_NT
+#define IPT_FRAME_NT 0  // frame-table gathers with the non-temporal hint
+#endif
+#ifndef IPT_COSA_NT
+#define IPT_COSA_NT 0  // CosineDdf r-table gathers with the non-temporal hint
+#endif
 #ifndef IPT_RAYGEN
 #define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
 #endif
@@ -1008,6 +1020,19 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     cs_c = tb.x;
                     cs_s = tb.y;
                 }
+            } else if (IPT_COSB_INLINE) {
+                // (cos phi, sin phi) computed (the table kernel's own code): one
+                // table line per cosine sample instead of two
+                if (IPT_COSA_INLINE)  // r too: no table line at all
+                    tr = sinf_small_(acosf_(sqrt_inrange_(u01(gi_a << 8))));
+                else if (IPT_COSA_NT)
+                    tr = __builtin_nontemporal_load(&kp.cos_a[gcos ? gi_a : 0u]);
+                else
+                    tr = kp.cos_a[gcos ? gi_a : 0u];
+                float sp, cp;
+                sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
+                cs_c = cp;
+                cs_s = sp;
             } else {
                 tr = kp.cos_a[gcos ? gi_a : 0u];
                 const float2 tb = kp.cos_b[gcos ? gi_b : 0u];
@@ -1686,7 +1711,14 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     const uint32_t u = f2u(to.z), mz = u & 0x7fffffffu;
                     pfok = mz - kFrameTabLo <= kFrameTabSpan;
                     if (pfok) {
+#if IPT_FRAME_NT
+                        typedef float f2v __attribute__((ext_vector_type(2)));
+                        const f2v ev = __builtin_nontemporal_load(
+                            reinterpret_cast<const f2v*>(&kp.frame_sc[((mz - kFrameTabLo) << 1) | (u >> 31)]));
+                        const float2 e = make_float2(ev.x, ev.y);
+#else
                         const float2 e = kp.frame_sc[((mz - kFrameTabLo) << 1) | (u >> 31)];
+#endif
                         pfs = e.x;
                         pfc = e.y;
                         pto = to;
