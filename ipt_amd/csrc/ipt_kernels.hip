@@ -213,6 +213,9 @@ struct KParams {
 #ifndef IPT_COSB_INLINE
 #define IPT_COSB_INLINE 1  // (cos phi, sin phi) of CosineDdf computed instead of gathered (+11 % C2)
 #endif
+#ifndef IPT_COSB_INLINE_RES
+#define IPT_COSB_INLINE_RES 1  // the same in the resumable (sphere-list, many-light) instances
+#endif
 #ifndef IPT_COSA_INLINE
 #define IPT_COSA_INLINE 0  // with IPT_COSB_INLINE: CosineDdf's r = sin(acos(sqrt(u1))) computed too
 #endif
@@ -841,6 +844,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     // a step costs the budget, not the longest walk of the workgroup.
     constexpr bool kRes = resumable_geom(GEOM);
     constexpr bool kResL = resumable_lights(LMODE, GEOM);
+    // the frame-entry prefetch pays where every lane iterates every step; in the
+    // resumable instances (lanes parked in walks) it measured -5 % on C5
+    constexpr int kFramePf = (kRes || kResL) ? 0 : IPT_FRAME_PF;
     bool tracing = false;  // a resumable walk (sphere list or light BVH) is in progress
     float xlmix = 0.0f;    // light walk: the running UnionDdf light sum
     vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
@@ -970,7 +976,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             }
         }
         };
-        if (IPT_FRAME_PF != 3) pop_node();
+        if (kFramePf != 3) pop_node();
 
         IPT_STAMP_AT(2);  // finalize + pop
         // the current node's frame normal (frame build below)
@@ -1016,9 +1022,16 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             if constexpr (kRes || kResL) {
                 if (ran && gcos) {
                     tr = kp.cos_a[gi_a];
-                    const float2 tb = kp.cos_b[gi_b];
-                    cs_c = tb.x;
-                    cs_s = tb.y;
+                    if (IPT_COSB_INLINE_RES) {
+                        float sp, cp;
+                        sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
+                        cs_c = cp;
+                        cs_s = sp;
+                    } else {
+                        const float2 tb = kp.cos_b[gi_b];
+                        cs_c = tb.x;
+                        cs_s = tb.y;
+                    }
                 }
             } else if (IPT_COSB_INLINE) {
                 // (cos phi, sin phi) computed (the table kernel's own code): one
@@ -1127,7 +1140,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     // gathers in their latency-bound walks)
                     vec3 to;
                     float fs = 0.0f, fc = 0.0f;
-                    if (IPT_FRAME_PF == 3) {
+                    if (kFramePf == 3) {
                         // `to` and its frame-table entry, prepared at the end of
                         // the previous step (pfok: `to` inside the table's range)
                         to = pto;
@@ -1141,7 +1154,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                                 keep_alive(fc);
                             }
                         pfok = false;
-                    } else if (IPT_FRAME_PF) {
+                    } else if (kFramePf) {
                         to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
                         // normally gathered at the end of the previous step
                         const bool have = f2u(to.z) == pfz;
@@ -1493,7 +1506,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         } else {
         // IPT_FRAME_PF == 2: the trace's results wait for resolve until the next
         // node's frame-table gather has been issued (see below)
-        constexpr bool kFramePf2 = IPT_FRAME_PF == 2 && IPT_FRAME_TAB && kFrameInrange && !kRes;
+        constexpr bool kFramePf2 = kFramePf == 2 && IPT_FRAME_TAB && kFrameInrange;
         bool rs_do = false, rs_has_li = false;
         float rs_t = inf_(), rs_mult = 0.0f, rs_li_pow = 0.0f;
         int rs_prim = -1;
@@ -1700,7 +1713,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             }
         }
         }  // !kResL
-        if constexpr (IPT_FRAME_PF == 3) {
+        if constexpr (kFramePf == 3) {
             pop_node();
             if constexpr (IPT_FRAME_TAB && kFrameInrange) {
                 // the frame the lane builds in the next step (a sphere node
@@ -1726,7 +1739,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
             }
         }
-        if constexpr (IPT_FRAME_PF == 1 && IPT_FRAME_TAB && kFrameInrange) {
+        if constexpr (kFramePf == 1 && IPT_FRAME_TAB && kFrameInrange) {
             // the node current at the next step and whether its frame is built
             // then: a sphere node pushed this step, or the pop target (the first
             // unfinished ancestor, as the pop computes it) when this node has run
