@@ -248,7 +248,8 @@ def main():
         traffic = None
         traffic_src = None
         cos_samples = cnt["iterations"] - cnt["light_samples"]
-        path_alg_bytes = roofline.path_bytes(total_paths // world // args.steps, cos_samples // world // args.steps)
+        path_alg_bytes = roofline.path_bytes(total_paths // world // args.steps, cos_samples // world // args.steps,
+                                             cnt["sphere_frames"] // world // args.steps)
         pmc_file = ROOT / "profiles" / "pmc_latest.json"
         if pmc_file.exists():
             try:
@@ -293,11 +294,13 @@ def main():
             "reference_scan_ops_per_path": (roofline.reference_scan_ops(cnt, len(desc.get("spheres", [])))
                                             / cnt["paths"]
                                             if cnt["bvh_nodes"] or cnt["light_nodes"] else None),
-            "note": ("hbm: algorithmic bytes of one path launch (5 B radiance + drift code per "
-                     "path, 16 B of CosineDdf table gathers per cosine-sampled iteration) / "
-                     "HIP-event launch time; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per "
-                     "launch of the same config (random 8-byte gathers move 64-byte lines: "
-                     "~8x the algorithmic bytes, measured cheaper than recomputing). valu: "
+            "note": ("hbm: algorithmic bytes of one path launch (5 B radiance + drift code and "
+                     "the 32 B raygen record per path, 4 B CosineDdf r gather per cosine-sampled "
+                     "iteration, 8 B frame-table gather per sphere frame) / HIP-event launch "
+                     "time; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per launch of the same "
+                     "config (random 4-8 byte gathers move 64-byte lines). The kernel is bound "
+                     "by instruction issue and gather latency (L2 requests per path), "
+                     "DESIGN.md section 6. valu: "
                      "algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
                      "counters) / launch time against the VALU issue peak 256CU x 4 SIMD32 x "
                      "2.4GHz -- the binding resource (no MFMA shape; HBM far from peak)"),

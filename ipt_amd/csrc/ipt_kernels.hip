@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     uint32_t pfz = 0xffffffffu;
     vec3 pto = v3(0, 0, 0);  // IPT_FRAME_PF == 3: the prepared frame's `to`
     bool pfok = false;
-    unsigned long long unit = 0;
+    uint32_t unit = 0;  // < 2^32 per launch (checked by the host)
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
     vec3 tpos = v3(0, 0, 0);
@@ -898,7 +898,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (my >= kp.total_units) {
                     active = false;
                 } else {
-                    unit = my;
+                    unit = (uint32_t)my;
                     has_path = true;
                     fresh = true;
                 }

@@ -1,9 +1,9 @@
 """Algorithmic cost model of the hot path and gfx950 peaks.
 
-The path kernel is FP32-VALU / divergence bound (no MFMA; its HBM traffic is
-the radiance output, 5 B per path, and the CosineDdf table gathers, 16 B per
-cosine-sampled iteration: ~1.7 KB per path at a fraction of 8 TB/s), so its
-roofline is the VALU issue rate. The op count
+The path kernel is bound by instruction issue and the latency of its random
+table gathers (no MFMA; its HBM traffic is the radiance output, the raygen
+records and the CosineDdf / frame-table gathers: ~0.6 KB per path at a
+fraction of 8 TB/s), so its roofline is the VALU issue rate. The op count
 is ALGORITHMIC: the reference's own arithmetic per event, counted as written
 (no credit for work the GPU kernel avoids, e.g. precomputed wall frames), with
 each transcendental (acos, sin, cos) at 20 op-eq. Event counts come from the
@@ -83,10 +83,12 @@ def accumulate_bytes(n_dest_pixels: int, spp: int, with_sums: bool = True,
     return n_dest_pixels * (4 * spp + 2 * state)
 
 
-def path_bytes(paths: int, cosine_samples: int = 0) -> int:
-    """Algorithmic HBM bytes of one path launch: 4 B radiance + 1 B drift code
-    written per path, plus the two 8-byte CosineDdf table entries gathered per
-    cosine-sampled iteration (the 2 x 128 MiB tables exceed L2 and, with the
-    radiance stream, the 256 MiB Infinity Cache; scene data is a few hundred
-    bytes, read once per CU)."""
-    return 5 * paths + 16 * cosine_samples
+def path_bytes(paths: int, cosine_samples: int = 0, frame_builds: int = 0) -> int:
+    """Algorithmic HBM bytes of one path launch, as the kernel moves them: 4 B
+    radiance + 1 B drift code written and the 32 B raygen record read per path,
+    the 4-byte CosineDdf r entry gathered per cosine-sampled iteration (64 MiB
+    table; (cos phi, sin phi) is computed in-lane since round 2), and the 8-byte
+    frame-table entry gathered per sphere-node frame build (1 GiB table; pushes
+    counted, the ~30 % rebuilds after pops are not). Scene data is a few hundred
+    bytes, read once per workgroup."""
+    return (5 + 32) * paths + 4 * cosine_samples + 8 * frame_builds
