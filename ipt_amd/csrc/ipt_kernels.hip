@@ -225,6 +225,9 @@ struct KParams {
 #ifndef IPT_COSA_NT
 #define IPT_COSA_NT 0  // CosineDdf r-table gathers with the non-temporal hint
 #endif
+#ifndef IPT_LIGHT_AXIS
+#define IPT_LIGHT_AXIS 1  // axis-aligned single-light instances (kLightsOneA10/A01)
+#endif
 #ifndef IPT_RAYGEN
 #define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
 #endif
@@ -603,7 +606,11 @@ __host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds
 // Where the lights live during the step loop (compile time, so that no
 // generic/flat pointer is ever formed: a flat load would make the compiler
 // wait for every outstanding radiance store).
-enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3, kLightsAny = 4 };
+enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3, kLightsAny = 4, kLightsOneA10 = 5, kLightsOneA01 = 6 };
+// kLightsOneA10 / A01: the single light is an axis-aligned AreaLight
+// (axis_aligned_light, ipt_path.h) with x_axis along y and y_axis along x
+// (A10, sample_scenes[0]'s light) or along x and y (A01), normal along z
+__host__ __device__ constexpr bool one_light(int lm) { return lm == kLightsOne || lm == kLightsOneA10 || lm == kLightsOneA01; }
 // kLightsAny: global-memory lights of any type (sphere, point, outer lights
 // present); the other modes are AreaLight-only.
 
@@ -618,17 +625,17 @@ struct LightSet {
     LightDev one;
     float w0, c0, c1;
     __device__ __forceinline__ const LightDev& light(int i) const {
-        if (LMODE == kLightsOne) return one;
+        if (one_light(LMODE)) return one;
         if (LMODE == kLightsLds) return lds[i];
         return glob[i];  // kLightsGlobal, kLightsAny
     }
     __device__ __forceinline__ float weight(int i) const {
-        if (LMODE == kLightsOne) return w0;
+        if (one_light(LMODE)) return w0;
         if (LMODE == kLightsLds || LMODE == kLightsGlobal) return wl[i];
         return wg[i];
     }
     __device__ __forceinline__ float cdf(int i) const {
-        if (LMODE == kLightsOne) return i == 0 ? c0 : c1;
+        if (one_light(LMODE)) return i == 0 ? c0 : c1;
         if (LMODE == kLightsLds || LMODE == kLightsGlobal) return cl[i];
         return cg[i];
     }
@@ -777,7 +784,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     LS.cl = LMODE == kLightsGlobal ? gl_lds + kp.n_lights + 1 : cdf_lds;
     LS.wg = kp.weights;
     LS.cg = kp.cdf;
-    if (LMODE == kLightsOne) {
+    if (one_light(LMODE)) {
         LS.one = kp.lights[0];
         if (IPT_LV & 1) { vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y); }
         if (IPT_LV & 2) { vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]); }
@@ -786,6 +793,23 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         LS.c0 = kp.cdf[0];
         LS.c1 = kp.cdf[1];
     }
+
+    // this instance's light functions (axis-aligned single light: the reduced
+    // forms of ipt_path.h, exact where observed)
+    auto ltrace = [&](const LightDev& L, vec3 o, vec3 d, vec3* hp, vec3* hn) -> bool {
+        if constexpr (LMODE == kLightsOneA10) return light_trace_ax<1, 0>(L, o, d, hp, hn);
+        else if constexpr (LMODE == kLightsOneA01) return light_trace_ax<0, 1>(L, o, d, hp, hn);
+        else return light_trace<LMODE == kLightsAny>(L, o, d, hp, hn);
+    };
+    auto lpdf = [&](const LightDev& L, vec3 o, bool h, vec3 hp, vec3 hn) -> float {
+        if constexpr (LMODE == kLightsOneA10 || LMODE == kLightsOneA01) return light_pdf_ax<2>(L, o, h, hp, hn);
+        else return light_pdf(L, o, h, hp, hn);
+    };
+    auto lsample = [&](const LightDev& L, vec3 o, float a, float b) -> vec3 {
+        if constexpr (LMODE == kLightsOneA10) return light_sample_dir_ax<1, 0>(L, o, a, b);
+        else if constexpr (LMODE == kLightsOneA01) return light_sample_dir_ax<0, 1>(L, o, a, b);
+        else return light_sample_dir<LMODE == kLightsAny>(L, o, a, b);
+    };
 
     // the sphere grid walk's parameters (kRes instances)
     KParams kg = kp;
@@ -800,7 +824,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     }
     const int lane = tid & 63;
     const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int nl = (IPT_NL1 && LMODE == kLightsOne) ? 1 : kp.n_lights;
+    const int nl = (IPT_NL1 && one_light(LMODE)) ? 1 : kp.n_lights;
     const float w_sdf = kp.weights[nl];
     const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
     // n at every depth is n_rays >> d; when n_rays is a power of two, res/n ==
@@ -1046,6 +1070,12 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
                 cs_c = cp;
                 cs_s = sp;
+                if (IPT_ABL == 8) {
+                    float sq, cq;
+                    sincosf_small_(two_pi_times(u01(gi_b << 8)) + kp.abl_zero, &sq, &cq);
+                    keep_alive(sq);
+                    keep_alive(cq);
+                }
             } else {
                 tr = kp.cos_a[gcos ? gi_a : 0u];
                 const float2 tb = kp.cos_b[gcos ? gi_b : 0u];
@@ -1072,7 +1102,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             const uint32_t j = k - 4 * blk;
             const float r = u01(win_at(w, j));
             int c = 0;
-            if (LMODE == kLightsOne) {
+            if (one_light(LMODE)) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
             } else if ((LMODE == kLightsGlobal || LMODE == kLightsAny) && kp.cdf_bsearch) {
                 // first c with r < cdf[c] (else nl+1): the scan's answer on a
@@ -1175,6 +1205,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                         // could decide a zero's sign take the exact build
                         bool ok;
                         f = make_frame_sc_fast(to, fs, fc, ok);
+                        if (IPT_ABL == 10) {
+                            bool ok2;
+                            keep_alive(make_frame_sc_fast(to, fs + kp.abl_zero, fc, ok2));
+                        }
                         if (__builtin_expect(__any(!ok), 0))
                             if (!ok) f = make_frame_sc<kFrameInrange>(to, fs, fc);
                     } else {
@@ -1265,19 +1299,20 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // one is selected (a mixed wave runs both anyway), so the CosineDdf
         // gathers have an unconditional consumer and stay unconditional loads
         vec3 dir_bf = v3(0, 0, 0);
-        if constexpr (LMODE == kLightsOne) {
+        if constexpr (one_light(LMODE)) {
             Frame fm;
             fm.m0 = v3(frc[0 * kFrameStride], frc[1 * kFrameStride], frc[2 * kFrameStride]);
             fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
             fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
             const vec3 cdir = frame_apply(fm, v3(tr * cs_c, tr * cs_s, sqrt_inrange_(u1)));
-            const vec3 ldir = light_sample_dir<false>(LS.one, tpos, u1, u2);
+            const vec3 ldir = lsample(LS.one, tpos, u1, u2);
+            if (IPT_ABL == 7) keep_alive(lsample(LS.one, tpos, u1 + kp.abl_zero, u2));
             const vec3 zero = v3(0, 0, 0);
             dir_bf = pick < nl ? ldir : (pick == nl ? cdir : zero);
         }
         if (iter_lane) {
             vec3 dir = v3(0, 0, 0);
-            if (LMODE == kLightsOne) {
+            if (one_light(LMODE)) {
                 dir = dir_bf;
                 if (COUNT && pick < nl) ++c_lsamp;
             } else if (pick < nl) {
@@ -1522,14 +1557,14 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             auto light_step = [&](int l) {
                 const LightDev& L = LS.light(l);
                 vec3 hp, hn;
-                const bool h = light_trace<LMODE == kLightsAny>(L, ro, rd, &hp, &hn);
+                const bool h = ltrace(L, ro, rd, &hp, &hn);
                 if (IPT_ABL == 4) {
                     vec3 hq, hm;
-                    const bool h2 = light_trace<LMODE == kLightsAny>(L, ro, rd * (1.0f + kp.abl_zero), &hq, &hm);
-                    keep_alive(light_pdf(L, ro, h2, hq, hm));
+                    const bool h2 = ltrace(L, ro, rd * (1.0f + kp.abl_zero), &hq, &hm);
+                    keep_alive(lpdf(L, ro, h2, hq, hm));
                 }
                 if (COUNT) ++c_ltest;
-                if (is_iter) lmix += LS.weight(l) * light_pdf(L, ro, h, hp, hn);
+                if (is_iter) lmix += LS.weight(l) * lpdf(L, ro, h, hp, hn);
                 if (h && (!has_li || longer(li_pos - ro, hp - ro))) {
                     has_li = true;
                     li_pos = hp;
@@ -2174,6 +2209,7 @@ struct ipt_ctx {
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
     bool any_round_light = false;
+    int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
     int bpc_override = 0;
     int lnodes_lds = 1;  // stage the light BVH in LDS (IPT_LNODES_LDS=0: global memory)
     vec3 cam_pos, cam_dir, cam_right, cam_up;
@@ -2372,12 +2408,12 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
 #define IPT_C2_ONLY 0
 #endif
 #ifndef IPT_C2_LMODE
-#define IPT_C2_LMODE kLightsOne
+#define IPT_C2_LMODE kLightsOneA10
 #endif
 template <int MAXSUSP, bool COUNT, int LMODE>
 int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     if constexpr (IPT_C2_ONLY != 0) {
-        if (MAXSUSP != 4 || LMODE != kLightsOne || kp.geometry_kind != IPT_GEOM_SPHERE_IN_BOX)
+        if (MAXSUSP != 4 || LMODE != IPT_C2_LMODE || kp.geometry_kind != IPT_GEOM_SPHERE_IN_BOX)
             return fail(ctx, IPT_E_UNSUPPORTED, "IPT_C2_ONLY experiment build");
         return launch_path4<4, COUNT, IPT_C2_LMODE, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
     } else {
@@ -2394,7 +2430,11 @@ int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
 template <int MAXSUSP, bool COUNT>
 int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     if (ctx->any_round_light) return launch_path3<MAXSUSP, COUNT, kLightsAny>(ctx, kp, st);
-    if (kp.n_lights == 1) return launch_path3<MAXSUSP, COUNT, kLightsOne>(ctx, kp, st);
+    if (kp.n_lights == 1) {
+        if (ctx->light_axis == 1) return launch_path3<MAXSUSP, COUNT, kLightsOneA10>(ctx, kp, st);
+        if (ctx->light_axis == 2) return launch_path3<MAXSUSP, COUNT, kLightsOneA01>(ctx, kp, st);
+        return launch_path3<MAXSUSP, COUNT, kLightsOne>(ctx, kp, st);
+    }
     if (kp.n_lights <= kLdsLights) return launch_path3<MAXSUSP, COUNT, kLightsLds>(ctx, kp, st);
     return launch_path3<MAXSUSP, COUNT, kLightsGlobal>(ctx, kp, st);
 }
@@ -2762,6 +2802,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->n_light_nodes = lnodes.empty() ? 0 : n_lnodes;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
     ctx->any_round_light = any_round;
+    ctx->light_axis = (nl == 1 && !any_round && IPT_LIGHT_AXIS) ? axis_aligned_light(L[0]) : 0;
     ctx->d_bvh_nodes = n_bvh_nodes.release();
     ctx->d_bvh_prims = n_bvh_prims.release();
     ctx->n_nodes = 0;

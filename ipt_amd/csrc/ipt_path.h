@@ -415,6 +415,96 @@ IPT_HD vec3 light_sample_dir(const LightDev& L, vec3 o, float u1, float u2raw) {
     return dir;
 }
 
+// ---------------------------------------------- axis-aligned single AreaLight
+// An AreaLight whose x_axis lies along coordinate axis XA, y_axis along YA and
+// whose normal (hence cross(x, y)) lies along NA = 3 - XA - YA, with every
+// other component of x, y, n and of the inverse matrix's coordinate rows an
+// exact (signed) zero and every component of the corner P non-zero (host-
+// checked: axis_aligned_light). Then every product with a zero component in the
+// reference's dot/mul/sample expressions is a signed zero added to a term
+// that is either non-zero (so it is an exact no-op) or compared against 0/1
+// only (so the zero's sign cannot matter): the terms below are exactly the
+// generic functions' results wherever those are observed.
+template <int I>
+IPT_HD float comp(vec3 v) {
+    return I == 0 ? v.x : (I == 1 ? v.y : v.z);
+}
+// light_trace (AreaLight::traceRay, lighting.cpp:107-144), n.d and n.(P-o)
+// reduced to their one non-zero term (a zero's sign only meets the |.| < 1e-6,
+// > 0 and t < 1e-6 rejections), coord = inverse*rel reduced to the rows' one
+// non-zero term each (compared with 0 and 1 only)
+template <int XA, int YA>
+IPT_HD bool light_trace_ax(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* nrm) {
+    constexpr int NA = 3 - XA - YA;
+    const float n_dir = comp<NA>(L.n) * comp<NA>(d);
+    const float t = div_(comp<NA>(L.n) * (comp<NA>(L.P) - comp<NA>(o)), n_dir);
+    const vec3 rel = (o + d * t) - L.P;
+    const float cx = comp<0>(L.inv.c[XA]) * comp<XA>(rel);
+    const float cy = comp<1>(L.inv.c[YA]) * comp<YA>(rel);
+    const bool in = L.type == 0 ? (cx >= 0.0f) & (cx <= 1.0f) & (cy >= 0.0f) & (cy <= 1.0f)
+                                : (cx >= 0.0f) & (cy >= 0.0f) & (cx + cy <= 1.0f);
+    *hit = L.P + rel;
+    *nrm = L.n;
+    return !(lt_1em6(fabs_(n_dir)) | (n_dir > 0.0f)) & !lt_1em6(t) & in;
+}
+// light_pdf (DdfFromLight::value) with cosinus = dot(n, -normalize(hit - o))
+// reduced to its one term (never a zero on a hit: |n.d| >= 1e-6 there)
+template <int NA>
+IPT_HD float light_pdf_ax(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nrm) {
+    if (!has) return 0.0f;
+    const vec3 ho = hit - o;
+    const float decay = dot(ho, ho);
+    const float s = div_(1.0f, sqrt_(decay));  // normalize's 1/sqrt(dot(v,v)) (same dot)
+    const float cosinus = comp<NA>(nrm) * -(comp<NA>(ho) * s);
+    const float p = div_(div_(decay, cosinus), L.area);
+    return cosinus < 0.0f ? 0.0f : p;
+}
+// light_sample_dir (DdfFromLight::sample via AreaLight::sample): pos =
+// (x*u1 + y*u2) + P keeps one product per component (P's components are
+// non-zero, so a zero product is an exact no-op), cosinus one term (compared
+// with 1e-5 only)
+template <int XA, int YA>
+IPT_HD vec3 light_sample_dir_ax(const LightDev& L, vec3 o, float u1, float u2raw) {
+    constexpr int NA = 3 - XA - YA;
+    const float u2 = u2raw * (L.type == 1 ? 1.0f - u1 : 1.0f);
+    float pc[3];
+    pc[XA] = comp<XA>(L.x) * u1 + comp<XA>(L.P);
+    pc[YA] = comp<YA>(L.y) * u2 + comp<YA>(L.P);
+    pc[NA] = comp<NA>(L.P);
+    const vec3 dir = normalize(v3(pc[0], pc[1], pc[2]) - o);
+    const float cosinus = comp<NA>(L.n) * -comp<NA>(dir);
+    if (cosinus < 1e-5f) return v3(0.0f, 0.0f, 0.0f);
+    return dir;
+}
+// Host check of the conditions above; returns 1 + index of the (XA, YA) pair
+// in {(1,0), (0,1)} (normal along z), else 0 (generic code).
+inline int axis_aligned_light(const LightDev& L) {
+    if (L.type != 0 && L.type != 1) return 0;
+    auto z = [](float f) { return (f2u(f) & 0x7fffffffu) == 0u; };
+    auto one_nz = [&](vec3 v, int a) {
+        const float c[3] = {v.x, v.y, v.z};
+        for (int i = 0; i < 3; ++i)
+            if ((i == a) == z(c[i])) return false;
+        return true;
+    };
+    if (z(L.P.x) || z(L.P.y) || z(L.P.z)) return 0;
+    const int pairs[2][2] = {{1, 0}, {0, 1}};
+    for (int k = 0; k < 2; ++k) {
+        const int xa = pairs[k][0], ya = pairs[k][1], na = 3 - xa - ya;
+        if (!one_nz(L.x, xa) || !one_nz(L.y, ya) || !one_nz(L.n, na)) continue;
+        // inverse rows 0 and 1 (coord.x, coord.y): one non-zero term each
+        const float r0[3] = {L.inv.c[0].x, L.inv.c[1].x, L.inv.c[2].x};
+        const float r1[3] = {L.inv.c[0].y, L.inv.c[1].y, L.inv.c[2].y};
+        bool ok = true;
+        for (int i = 0; i < 3; ++i) {
+            if (i != xa && !z(r0[i])) ok = false;
+            if (i != ya && !z(r1[i])) ok = false;
+        }
+        if (ok) return 1 + k;
+    }
+    return 0;
+}
+
 // Light constructor derived fields: AreaLight (lighting.cpp:79-90) + the
 // per-call normal/power expressions of traceRay/sample; SphereLight /
 // InvertedSphereLight: area = 4.0*M_PI*radius*radius in f64 (lighting.h:

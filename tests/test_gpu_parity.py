@@ -359,3 +359,28 @@ def test_failed_upload_leaves_no_scene(gpu_ctx, oracle, monkeypatch, fail_at):
     gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
     assert np.array_equal(gc, oc)
     assert np.array_equal(_bits(gv), _bits(ov))
+
+
+@pytest.mark.parametrize("light", [
+    # x along y, y along x, facing down: sample_scenes[0]'s pattern (kLightsOneA10)
+    {"position": [-0.3, 0.2, 0.7], "x_axis": [0.0, 0.3, 0.0], "y_axis": [0.25, 0.0, 0.0], "power": 2.0, "type": 0},
+    # x along x, y along -y, facing down (kLightsOneA01)
+    {"position": [-0.2, 0.4, 0.6], "x_axis": [0.3, 0.0, 0.0], "y_axis": [0.0, -0.3, 0.0], "power": 1.0, "type": 0},
+    # triangle with the A10 pattern
+    {"position": [0.3, -0.5, 0.5], "x_axis": [0.0, 0.4, 0.0], "y_axis": [0.4, 0.0, 0.0], "power": 1.0, "type": 1},
+    # a corner component exactly 0: the generic code (the reduced forms need P != 0)
+    {"position": [0.0, -0.9, -0.15], "x_axis": [0.0, 0.2, 0.0], "y_axis": [0.2, 0.0, 0.0], "power": 1.0, "type": 0},
+    # facing up (A10 axes swapped sign): light seen from below only by its back
+    {"position": [0.1, -0.9, -0.6], "x_axis": [0.0, -0.2, 0.0], "y_axis": [0.2, 0.0, 0.0], "power": 1.0, "type": 0},
+])
+def test_axis_aligned_single_light_bit_exact(gpu_ctx, oracle, light):
+    """A single axis-aligned AreaLight runs the reduced light trace / pdf /
+    sample forms (light_trace_ax etc., ipt_path.h: the zero components'
+    products dropped where they are exact no-ops); the images must stay
+    bit-identical to the oracle's generic arithmetic, incl. the fallback cases."""
+    desc = scenes.make_scene_box()
+    desc["lights"] = [light]
+    p = capi.make_params(40, 32, 2, n_rays=16, depth_max=8)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
