@@ -225,6 +225,9 @@ struct KParams {
 #ifndef IPT_COSA_NT
 #define IPT_COSA_NT 0  // CosineDdf r-table gathers with the non-temporal hint
 #endif
+#ifndef IPT_LIGHT_INR
+#define IPT_LIGHT_INR 1  // ... with the range-free roots / quotients of light_ranges_box
+#endif
 #ifndef IPT_LIGHT_AXIS
 #define IPT_LIGHT_AXIS 1  // axis-aligned single-light instances (kLightsOneA10/A01)
 #endif
@@ -797,17 +800,17 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     // this instance's light functions (axis-aligned single light: the reduced
     // forms of ipt_path.h, exact where observed)
     auto ltrace = [&](const LightDev& L, vec3 o, vec3 d, vec3* hp, vec3* hn) -> bool {
-        if constexpr (LMODE == kLightsOneA10) return light_trace_ax<1, 0>(L, o, d, hp, hn);
-        else if constexpr (LMODE == kLightsOneA01) return light_trace_ax<0, 1>(L, o, d, hp, hn);
+        if constexpr (LMODE == kLightsOneA10) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
+        else if constexpr (LMODE == kLightsOneA01) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
         else return light_trace<LMODE == kLightsAny>(L, o, d, hp, hn);
     };
     auto lpdf = [&](const LightDev& L, vec3 o, bool h, vec3 hp, vec3 hn) -> float {
-        if constexpr (LMODE == kLightsOneA10 || LMODE == kLightsOneA01) return light_pdf_ax<2>(L, o, h, hp, hn);
+        if constexpr (LMODE == kLightsOneA10 || LMODE == kLightsOneA01) return light_pdf_ax<2, IPT_LIGHT_INR>(L, o, h, hp, hn);
         else return light_pdf(L, o, h, hp, hn);
     };
     auto lsample = [&](const LightDev& L, vec3 o, float a, float b) -> vec3 {
-        if constexpr (LMODE == kLightsOneA10) return light_sample_dir_ax<1, 0>(L, o, a, b);
-        else if constexpr (LMODE == kLightsOneA01) return light_sample_dir_ax<0, 1>(L, o, a, b);
+        if constexpr (LMODE == kLightsOneA10) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
+        else if constexpr (LMODE == kLightsOneA01) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
         else return light_sample_dir<LMODE == kLightsAny>(L, o, a, b);
     };
 
@@ -2802,7 +2805,11 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->n_light_nodes = lnodes.empty() ? 0 : n_lnodes;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
     ctx->any_round_light = any_round;
+    // the axis-aligned single-light instances also take the range-free roots
+    // and quotients: only where their ranges are proven (sphere-in-box scenes)
     ctx->light_axis = (nl == 1 && !any_round && IPT_LIGHT_AXIS) ? axis_aligned_light(L[0]) : 0;
+    if (ctx->light_axis && !(s->geometry_kind == IPT_GEOM_SPHERE_IN_BOX && light_ranges_box(L[0], 2, cam)))
+        ctx->light_axis = 0;
     ctx->d_bvh_nodes = n_bvh_nodes.release();
     ctx->d_bvh_prims = n_bvh_prims.release();
     ctx->n_nodes = 0;

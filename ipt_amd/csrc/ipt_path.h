@@ -433,11 +433,19 @@ IPT_HD float comp(vec3 v) {
 // reduced to their one non-zero term (a zero's sign only meets the |.| < 1e-6,
 // > 0 and t < 1e-6 rejections), coord = inverse*rel reduced to the rows' one
 // non-zero term each (compared with 0 and 1 only)
-template <int XA, int YA>
+//
+// INR: the scene's ranges are host-proven (light_ranges_box below), so these
+// quotients and roots take the range-free sequences (div_inrange_,
+// sqrt_inrange_: bit-identical in range, ipt_math.h). Where a quotient is out
+// of range its result is never observed (the hit is rejected or the lane's
+// pdf is not used), exactly as its IEEE value would not be.
+template <int XA, int YA, bool INR = false>
 IPT_HD bool light_trace_ax(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* nrm) {
     constexpr int NA = 3 - XA - YA;
     const float n_dir = comp<NA>(L.n) * comp<NA>(d);
-    const float t = div_(comp<NA>(L.n) * (comp<NA>(L.P) - comp<NA>(o)), n_dir);
+    // INR: |num| is 0 or in [2^-40, 2^41); |n_dir| >= 1e-6 wherever t is used
+    const float num = comp<NA>(L.n) * (comp<NA>(L.P) - comp<NA>(o));
+    const float t = INR ? div_inrange_(num, n_dir) : div_(num, n_dir);
     const vec3 rel = (o + d * t) - L.P;
     const float cx = comp<0>(L.inv.c[XA]) * comp<XA>(rel);
     const float cy = comp<1>(L.inv.c[YA]) * comp<YA>(rel);
@@ -449,21 +457,23 @@ IPT_HD bool light_trace_ax(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* n
 }
 // light_pdf (DdfFromLight::value) with cosinus = dot(n, -normalize(hit - o))
 // reduced to its one term (never a zero on a hit: |n.d| >= 1e-6 there)
-template <int NA>
+template <int NA, bool INR = false>
 IPT_HD float light_pdf_ax(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nrm) {
     if (!has) return 0.0f;
     const vec3 ho = hit - o;
     const float decay = dot(ho, ho);
-    const float s = div_(1.0f, sqrt_(decay));  // normalize's 1/sqrt(dot(v,v)) (same dot)
+    // INR on a hit: decay in [dmin^2, dmax^2], cosinus in [~1e-6, 1], area in range
+    const float s = INR ? div_inrange_(1.0f, sqrt_inrange_(decay))
+                        : div_(1.0f, sqrt_(decay));  // normalize's 1/sqrt(dot(v,v)) (same dot)
     const float cosinus = comp<NA>(nrm) * -(comp<NA>(ho) * s);
-    const float p = div_(div_(decay, cosinus), L.area);
+    const float p = INR ? div_inrange_(div_inrange_(decay, cosinus), L.area) : div_(div_(decay, cosinus), L.area);
     return cosinus < 0.0f ? 0.0f : p;
 }
 // light_sample_dir (DdfFromLight::sample via AreaLight::sample): pos =
 // (x*u1 + y*u2) + P keeps one product per component (P's components are
 // non-zero, so a zero product is an exact no-op), cosinus one term (compared
 // with 1e-5 only)
-template <int XA, int YA>
+template <int XA, int YA, bool INR = false>
 IPT_HD vec3 light_sample_dir_ax(const LightDev& L, vec3 o, float u1, float u2raw) {
     constexpr int NA = 3 - XA - YA;
     const float u2 = u2raw * (L.type == 1 ? 1.0f - u1 : 1.0f);
@@ -471,7 +481,8 @@ IPT_HD vec3 light_sample_dir_ax(const LightDev& L, vec3 o, float u1, float u2raw
     pc[XA] = comp<XA>(L.x) * u1 + comp<XA>(L.P);
     pc[YA] = comp<YA>(L.y) * u2 + comp<YA>(L.P);
     pc[NA] = comp<NA>(L.P);
-    const vec3 dir = normalize(v3(pc[0], pc[1], pc[2]) - o);
+    // INR: |pos - o| in [dmin, dmax] for every surface point o
+    const vec3 dir = INR ? normalize_inrange_(v3(pc[0], pc[1], pc[2]) - o) : normalize(v3(pc[0], pc[1], pc[2]) - o);
     const float cosinus = comp<NA>(L.n) * -comp<NA>(dir);
     if (cosinus < 1e-5f) return v3(0.0f, 0.0f, 0.0f);
     return dir;
@@ -503,6 +514,59 @@ inline int axis_aligned_light(const LightDev& L) {
         if (ok) return 1 + k;
     }
     return 0;
+}
+
+// Host proof of the INR ranges for an axis-aligned single AreaLight in
+// GeometrySphereInBox: every ray origin is the camera, a wall point (a hit of
+// the box planes: inside the cube up to rounding) or a sphere point (|p| =
+// 0.5 up to rounding). dmin (a lower bound of |light point - origin|) comes
+// from the light's bounding box against the wall planes, the sphere and the
+// camera; dmax from the cube and camera extents. Required: dmin >= 2^-8
+// (decay >= 2^-16; 1/sqrt, decay/cosinus and the sample's normalize in range),
+// dmax <= 2^8, area and |n| in [2^-16, 2^16], |P_NA| >= 2^-8 (a non-zero
+// P_NA - o_NA is then >= 2^-32, so t's numerator is 0 or in range).
+inline bool light_ranges_box(const LightDev& L, int na, const float cam[3]) {
+    float lo[3], hi[3];
+    const float P[3] = {L.P.x, L.P.y, L.P.z}, X[3] = {L.x.x, L.x.y, L.x.z}, Y[3] = {L.y.x, L.y.y, L.y.z};
+    for (int i = 0; i < 3; ++i) {
+        lo[i] = P[i] + (X[i] < 0.0f ? X[i] : 0.0f) + (Y[i] < 0.0f ? Y[i] : 0.0f);
+        hi[i] = P[i] + (X[i] > 0.0f ? X[i] : 0.0f) + (Y[i] > 0.0f ? Y[i] : 0.0f);
+    }
+    const double m = 1e-5;  // rounding slack of hit points and of the box above
+    double dmin = 1e30;
+    // wall planes x = +-1, y = +1, z = +-1 (GeometrySphereInBox.cpp:10-81)
+    const double walls[5][2] = {{0, 1}, {1, 1}, {2, 1}, {0, -1}, {2, -1}};
+    for (const auto& w : walls) {
+        const int a = (int)w[0];
+        const double v = w[1];
+        const double dd = (lo[a] > v) ? lo[a] - v : ((hi[a] < v) ? v - hi[a] : 0.0);
+        dmin = dd < dmin ? dd : dmin;
+    }
+    auto box_dist = [&](const double q[3]) {
+        double s2 = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            const double dd = q[i] < lo[i] ? lo[i] - q[i] : (q[i] > hi[i] ? q[i] - hi[i] : 0.0);
+            s2 += dd * dd;
+        }
+        return __builtin_sqrt(s2);
+    };
+    const double origin[3] = {0, 0, 0}, c[3] = {cam[0], cam[1], cam[2]};
+    const double ds = box_dist(origin) - 0.5;
+    dmin = ds < dmin ? ds : dmin;
+    const double dc = box_dist(c);
+    dmin = dc < dmin ? dc : dmin;
+    dmin -= m;
+    double ext = 1.0;
+    for (int i = 0; i < 3; ++i) {
+        const double e = __builtin_fabs(lo[i]) > __builtin_fabs(hi[i]) ? __builtin_fabs(lo[i]) : __builtin_fabs(hi[i]);
+        ext = e > ext ? e : ext;
+        ext = __builtin_fabs(cam[i]) > ext ? __builtin_fabs(cam[i]) : ext;
+    }
+    const double dmax = 2.0 * ext * 1.7320508 + m;
+    const float n[3] = {L.n.x, L.n.y, L.n.z};
+    const float pn = P[na];
+    return dmin >= 0x1p-8 && dmax <= 0x1p8 && L.area >= 0x1p-16f && L.area <= 0x1p16f &&
+           __builtin_fabs(n[na]) >= 0x1p-16f && __builtin_fabs(n[na]) <= 0x1p16f && __builtin_fabs(pn) >= 0x1p-8f;
 }
 
 // Light constructor derived fields: AreaLight (lighting.cpp:79-90) + the
