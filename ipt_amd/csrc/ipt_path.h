@@ -240,11 +240,46 @@ IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
     return t;
 }
 
+// The facing plane of axis a (sgn chosen so that sgn*d_a > 0 unless d_a is a
+// zero): dp = sgn*d_a equals |d_a| whenever |dp| >= 1e-6 (otherwise the test
+// misses either way), so `dp < 0` never decides, and 1 - sgn*o_a is one
+// rounding of an exact product, i.e. fma(-sgn, o_a, 1). Same t, same miss.
+#ifndef IPT_BOXPLANES
+#define IPT_BOXPLANES 1
+#endif
+template <bool INRANGE>
+IPT_HD float facing_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
+    const float dp = fabs_(da);
+    const float num = __builtin_fmaf(-sgn, oa, 1.0f);
+    const float t = INRANGE ? div_inrange_(num, dp) : div_(num, dp);
+    const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
+    const bool miss =
+        lt_1em6(dp) | (fabs_(px) > 1.0f) | (fabs_(py) > 1.0f) | (fabs_(pz) > 1.0f) | lt_1em6(t);
+    return miss ? inf_() : t;
+}
+
 // GeometrySphereInBox::traceRay (GeometrySphereInBox.cpp:10-81) nearest hit:
 // returns t (inf = miss) and the hit primitive: 0..4 = plane index in the
 // reference's order {+x,+y,+z,-x,-z}, 5 = the r=0.5 sphere.
 template <bool INRANGE = false>
 IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
+    if (IPT_BOXPLANES && IPT_BRANCHFREE) {
+        // a NaN direction fails every test (the reference returns no hit);
+        // the planes are computed regardless and the result selected at the end
+        const bool dnan = d.x + d.y + d.z != d.x + d.y + d.z;
+        const bool xp = d.x > 0.0f, zp = d.z > 0.0f;
+        float best = facing_plane_t<INRANGE>(o.x, d.x, xp ? 1.0f : -1.0f, o, d);
+        int bi = xp ? 0 : 3;
+        const float ty0 = facing_plane_t<INRANGE>(o.y, d.y, 1.0f, o, d);
+        const float ty = d.y > 0.0f ? ty0 : inf_();
+        if (ty < best || (ty == best && 1 < bi && ty != inf_())) { best = ty; bi = 1; }
+        const float tz = facing_plane_t<INRANGE>(o.z, d.z, zp ? 1.0f : -1.0f, o, d);
+        const int iz = zp ? 2 : 4;
+        if (tz < best || (tz == best && iz < bi && tz != inf_())) { best = tz; bi = iz; }
+        const bool none = dnan | (best == inf_());
+        *prim = none ? -1 : bi;
+        return dnan ? inf_() : best;
+    }
     float best = inf_();
     int bi = -1;
     if (d.x + d.y + d.z != d.x + d.y + d.z) {  // NaN direction: every test fails
