@@ -319,6 +319,18 @@ __device__ __forceinline__ uint32_t win_at(const Win8& w, uint32_t j) {
     return j < 4 ? lo : hi;
 }
 
+// w_j, w_(j+1), w_(j+2) for j in [0,4) (the prologue shifts the window as soon
+// as k leaves block blk, and a step consumes at most 3 draws): three 4-way
+// selects on j's two bits instead of three 6-way chains
+#ifndef IPT_WIN4
+#define IPT_WIN4 1
+#endif
+__device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    const bool b0 = (j & 1u) != 0u, b1 = (j & 2u) != 0u;
+    const uint32_t lo = b0 ? x1 : x0, hi = b0 ? x3 : x2;
+    return b1 ? hi : lo;
+}
+
 __device__ __forceinline__ void philox_fill(uint32_t& d0, uint32_t& d1, uint32_t& d2, uint32_t& d3,
                                             uint32_t blk, uint32_t pass, uint32_t pix, uint32_t k0,
                                             uint32_t k1) {
@@ -1102,8 +1114,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
                 need_b = false;
             }
-            const uint32_t j = k - 4 * blk;
-            const float r = u01(win_at(w, j));
+            const uint32_t j = IPT_WIN4 ? (k & 3u) : k - 4 * blk;
+            const float r = u01(IPT_WIN4 ? sel4(j, w.a0, w.a1, w.a2, w.a3) : win_at(w, j));
             int c = 0;
             if (one_light(LMODE)) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
@@ -1120,7 +1132,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             }
             pick = c;
             if (c <= nl) {
-                const uint32_t r1 = win_at(w, j + 1), r2 = win_at(w, j + 2);
+                const uint32_t r1 = IPT_WIN4 ? sel4(j, w.a1, w.a2, w.a3, w.b0) : win_at(w, j + 1);
+                const uint32_t r2 = IPT_WIN4 ? sel4(j, w.a2, w.a3, w.b0, w.b1) : win_at(w, j + 2);
                 u1 = u01(r1);
                 u2 = u01(r2);
                 if (c == nl) {

@@ -210,12 +210,24 @@ IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
 // affect the f32 rounding (see DESIGN.md "mixed precision").
 // BF: branch-free (the box's one sphere, hit by a large share of rays); the
 // sphere lists' tests stay branchy (most miss at the discriminant)
-template <bool BF = false>
+// INR (the box sphere, r = 0.5, |o| < 2^39): desc = 4*fl(A - B), A = fl(b*b),
+// B = fl(dot(o,o) - 0.25), and sd through the range-free root. B is 0 or
+// |B| >= 2^-26 (for dot(o,o) in [1/8, 1/2] the difference is exact and a
+// multiple of 2^-26), so a nonzero A - B is >= 2^-49 unless B = 0: 4*(A - B)
+// is then never subnormal and equals the reference's fl(4A - 4B). desc lies in
+// (0, 2^-96), outside the root's range, only when B = 0 and A < 2^-98, i.e.
+// |b| < 2^-48: sd < 2^-45 with either root, both roots fall below 1e-6 and the
+// test misses either way. desc is never -0 (A >= +0); desc < 2^84.
+#ifndef IPT_SPHERE_INR
+#define IPT_SPHERE_INR 1
+#endif
+template <bool BF = false, bool INR = false>
 IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
     const float b = dot(o, d);
-    const float desc = 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
+    const float desc = (INR && IPT_SPHERE_INR) ? 4.0f * (b * b - (dot(o, o) - radius * radius))
+                                               : 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
     if (BF) {
-        const float sd = sqrt_(desc);
+        const float sd = (INR && IPT_SPHERE_INR) ? sqrt_inrange_(desc) : sqrt_(desc);
         const float m2b = -2.0f * b;
         float t1 = (m2b - sd) * 0.5f;
         float t2 = (m2b + sd) * 0.5f;
@@ -312,7 +324,7 @@ template <bool INRANGE = false>
 IPT_HD float trace_box(vec3 o, vec3 d, int* prim) {
     int bi;
     float best = trace_box_planes_only<INRANGE>(o, d, &bi);
-    const float ts = sphere_t<IPT_BRANCHFREE>(0.5f, o, d);
+    const float ts = sphere_t<IPT_BRANCHFREE, INRANGE>(0.5f, o, d);
     if (ts < best) { best = ts; bi = 5; }
     *prim = bi;
     return best;
