@@ -259,6 +259,9 @@ IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
 #ifndef IPT_BOXPLANES
 #define IPT_BOXPLANES 1
 #endif
+#ifndef IPT_BOXSEL
+#define IPT_BOXSEL 1
+#endif
 template <bool INRANGE>
 IPT_HD float facing_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
     const float dp = fabs_(da);
@@ -284,10 +287,20 @@ IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
         int bi = xp ? 0 : 3;
         const float ty0 = facing_plane_t<INRANGE>(o.y, d.y, 1.0f, o, d);
         const float ty = d.y > 0.0f ? ty0 : inf_();
-        if (ty < best || (ty == best && 1 < bi && ty != inf_())) { best = ty; bi = 1; }
+        // the scan's "nearer, or as near with a lower index" as selects (bitwise
+        // on the comparisons: no short-circuit control flow)
+        if (IPT_BOXSEL) {
+            const bool take_y = (ty < best) | ((ty == best) & (1 < bi) & (ty != inf_()));
+            best = take_y ? ty : best;
+            bi = take_y ? 1 : bi;
+        } else if (ty < best || (ty == best && 1 < bi && ty != inf_())) { best = ty; bi = 1; }
         const float tz = facing_plane_t<INRANGE>(o.z, d.z, zp ? 1.0f : -1.0f, o, d);
         const int iz = zp ? 2 : 4;
-        if (tz < best || (tz == best && iz < bi && tz != inf_())) { best = tz; bi = iz; }
+        if (IPT_BOXSEL) {
+            const bool take_z = (tz < best) | ((tz == best) & (iz < bi) & (tz != inf_()));
+            best = take_z ? tz : best;
+            bi = take_z ? iz : bi;
+        } else if (tz < best || (tz == best && iz < bi && tz != inf_())) { best = tz; bi = iz; }
         const bool none = dnan | (best == inf_());
         *prim = none ? -1 : bi;
         return dnan ? inf_() : best;
