@@ -94,8 +94,8 @@ EXPORTED_SYMBOLS = (
 PROFILE_PHASES = ("step", "pop", "new_path", "iteration", "philox", "frame_worker",
                   "cosine_worker", "light_sample", "trace", "geometry", "push", "wg_step")
 # step segments of the IPT_STAMP diagnostic build (IPT_STAMP_AT ids)
-STAMP_SEGMENTS = ("tail", "refill", "pop", "new_path", "post_prologue_philox", "barrier_a",
-                  "workers", "barrier_b", "direction", "lights", "geometry")
+STAMP_SEGMENTS = ("loop_top", "refill", "pop_early", "pre_prologue", "prologue_philox_frame", "exit_test",
+                  "pop", "frame_prefetch", "new_path_direction", "lights", "mixture_geometry", "resolve_push")
 
 _lib = None
 

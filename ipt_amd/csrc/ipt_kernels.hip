@@ -325,6 +325,9 @@ __device__ __forceinline__ uint32_t win_at(const Win8& w, uint32_t j) {
 #ifndef IPT_WIN4
 #define IPT_WIN4 1
 #endif
+#ifndef IPT_POP2
+#define IPT_POP2 1  // the pop's LDS reads issued together (see pop_node)
+#endif
 __device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
     const bool b0 = (j & 1u) != 0u, b1 = (j & 2u) != 0u;
     const uint32_t lo = b0 ? x1 : x0, hi = b0 ? x3 : x2;
@@ -964,9 +967,52 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     v = n_pow2 ? r * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - d)) : r / (float)(kp.n_rays >> d);
                 return v;
             };
-            float v = fin_v(tres, tdepth);
             const uint32_t m = ~finm & ((1u << tdepth) - 1u);
             const int stop = m ? 31 - (int)__clz(m) : -1;
+            if (IPT_POP2) {
+                // every LDS read of the unwind issued before the first use -- the
+                // resumed level's six fields and the res/multiplier of the first
+                // two finished levels (addresses clamped to level 0 where a level
+                // does not exist; those values are not used) -- so that their
+                // latencies overlap instead of forming a chain; the outcomes as
+                // selects so that the loads have unconditional consumers
+                auto lvl = [&](int l) { return stk + (size_t)(l < 0 ? 0 : l) * kStackFields * kBlock + tid; };
+                const float* bs = lvl(stop);
+                const float s0 = bs[0 * kBlock], s1 = bs[1 * kBlock], s2 = bs[2 * kBlock];
+                const float s3 = bs[3 * kBlock], s4 = bs[4 * kBlock], s5 = bs[5 * kBlock];
+                const float* b1 = lvl(tdepth - 1);
+                const float r1 = b1[3 * kBlock], m1 = b1[4 * kBlock];
+                const float* b2 = lvl(tdepth - 2);
+                const float r2 = b2[3 * kBlock], m2 = b2[4 * kBlock];
+                auto fin_s = [&](float r, int d) {
+                    const float q = n_pow2 ? r * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - d))
+                                           : r / (float)(kp.n_rays >> (d < 0 ? 0 : d));
+                    return isfinite_(r) ? q : 0.0f;
+                };
+                float v = fin_s(tres, tdepth);
+                const float v1 = fin_s(r1 + (m1 * 1.0f) * v, tdepth - 1);
+                v = tdepth - 1 > stop ? v1 : v;
+                const float v2 = fin_s(r2 + (m2 * 1.0f) * v, tdepth - 2);
+                v = tdepth - 2 > stop ? v2 : v;
+                for (int l = tdepth - 3; l > stop; --l) {
+                    const float* b = lvl(l);
+                    v = fin_v(b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v, l);
+                }
+                const bool resume = stop >= 0;
+                const int meta = __float_as_int(s5);
+                tpos = resume ? v3(s0, s1, s2) : tpos;
+                tres = resume ? s3 + (s4 * 1.0f) * v : tres;  // res += multiplier*albedo*ray_power
+                ti = resume ? meta & 0xff : ti;
+                tkind = resume ? meta >> 8 : tkind;
+                need_frame = resume ? (meta >> 8) >= 5 && fdepth != stop : need_frame;
+                tdepth = resume ? stop : tdepth;
+                if (!resume) {
+                    kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
+                    has_path = false;
+                }
+                return;
+            }
+            float v = fin_v(tres, tdepth);
             for (int l = tdepth - 1; l > stop; --l) {
                 const float* b = stk + (size_t)l * kStackFields * kBlock + tid;
                 v = fin_v(b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v, l);
@@ -1694,6 +1740,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
             }
         }
+        IPT_STAMP_AT(11);  // resolve + push
         if constexpr (kFramePf2) {
             // the node current at the next step and whether its frame is built
             // then -- a sphere node this ray pushes (resolve's decision, computed
@@ -1766,6 +1813,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }  // !kResL
         if constexpr (kFramePf == 3) {
             pop_node();
+            IPT_STAMP_AT(6);  // pop (end of step)
             if constexpr (IPT_FRAME_TAB && kFrameInrange) {
                 // the frame the lane builds in the next step (a sphere node
                 // pushed in this step, or popped back to with its column
@@ -1789,6 +1837,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     }
                 }
             }
+            IPT_STAMP_AT(7);  // next frame's `to` + table gather
         }
         if constexpr (kFramePf == 1 && IPT_FRAME_TAB && kFrameInrange) {
             // the node current at the next step and whether its frame is built
