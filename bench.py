@@ -299,8 +299,8 @@ def main():
                      "iteration, 8 B frame-table gather per sphere frame) / HIP-event launch "
                      "time; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per launch of the same "
                      "config (random 4-8 byte gathers move 64-byte lines). The kernel is bound "
-                     "by instruction issue and gather latency (L2 requests per path), "
-                     "DESIGN.md section 6. valu: "
+                     "by instruction issue (VALU work and the exec-mask bookkeeping of its "
+                     "branches; the gather latency is hidden), DESIGN.md sections 4.3 and 6. valu: "
                      "algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
                      "counters) / launch time against the VALU issue peak 256CU x 4 SIMD32 x "
                      "2.4GHz -- the binding resource (no MFMA shape; HBM far from peak)"),
