@@ -187,6 +187,11 @@ struct KParams {
     const BvhNode* __restrict__ light_nodes;   // n_light_nodes > 0: light BVH over index ranges
     int n_light_nodes;
     int lnodes_lds;                       // light BVH staged in LDS (kLightsGlobal)
+    // kLightsGridA10/A01: coplanar axis-aligned lights on a lattice (LightGrid)
+    const int* __restrict__ lgrid;        // [lg_nu * lg_nv] light index per cell, -1 = none
+    int lg_nu, lg_nv;
+    float lg_u0, lg_v0, lg_icw, lg_ich;   // cell coordinates: (q - u0) * icw
+    float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
@@ -230,6 +235,9 @@ struct KParams {
 #endif
 #ifndef IPT_LIGHT_AXIS
 #define IPT_LIGHT_AXIS 1  // axis-aligned single-light instances (kLightsOneA10/A01)
+#endif
+#ifndef IPT_LIGHT_GRID
+#define IPT_LIGHT_GRID 1  // coplanar light lattices by cell lookup (kLightsGridA10/A01)
 #endif
 #ifndef IPT_RAYGEN
 #define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
@@ -624,7 +632,14 @@ __host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds
 // Where the lights live during the step loop (compile time, so that no
 // generic/flat pointer is ever formed: a flat load would make the compiler
 // wait for every outstanding radiance store).
-enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3, kLightsAny = 4, kLightsOneA10 = 5, kLightsOneA01 = 6 };
+enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3, kLightsAny = 4, kLightsOneA10 = 5, kLightsOneA01 = 6,
+       kLightsGridA10 = 7, kLightsGridA01 = 8 };
+// kLightsGridA10 / A01: many AreaLights, all axis-aligned with the same axis
+// pattern, sharing their plane and lying on a lattice, one per cell
+// (light_grid_build): a ray's lights are found by its plane point's cell(s)
+// instead of the light BVH walk; weights and CDF staged as kLightsGlobal.
+__host__ __device__ constexpr bool grid_lights(int lm) { return lm == kLightsGridA10 || lm == kLightsGridA01; }
+__host__ __device__ constexpr bool global_lights(int lm) { return lm == kLightsGlobal || grid_lights(lm); }
 // kLightsOneA10 / A01: the single light is an axis-aligned AreaLight
 // (axis_aligned_light, ipt_path.h) with x_axis along y and y_axis along x
 // (A10, sample_scenes[0]'s light) or along x and y (A01), normal along z
@@ -649,12 +664,12 @@ struct LightSet {
     }
     __device__ __forceinline__ float weight(int i) const {
         if (one_light(LMODE)) return w0;
-        if (LMODE == kLightsLds || LMODE == kLightsGlobal) return wl[i];
+        if (LMODE == kLightsLds || global_lights(LMODE)) return wl[i];
         return wg[i];
     }
     __device__ __forceinline__ float cdf(int i) const {
         if (one_light(LMODE)) return i == 0 ? c0 : c1;
-        if (LMODE == kLightsLds || LMODE == kLightsGlobal) return cl[i];
+        if (LMODE == kLightsLds || global_lights(LMODE)) return cl[i];
         return cg[i];
     }
 };
@@ -783,12 +798,14 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     }
     if (cand_in_lds)
         for (int i = tid; i < kp.n_cand; i += kBlock) cand_lds[i] = kp.cand_rows[i];
-    if (LMODE == kLightsGlobal) {
+    if (global_lights(LMODE)) {
         for (int i = tid; i <= kp.n_lights; i += kBlock) {
             gl_lds[i] = kp.weights[i];
             gl_lds[kp.n_lights + 1 + i] = kp.cdf[i];
         }
-        if (kp.lnodes_lds) {
+        if (grid_lights(LMODE))
+            for (int i = tid; i < kp.lg_nu * kp.lg_nv; i += kBlock) reinterpret_cast<int*>(lnodes_lds)[i] = kp.lgrid[i];
+        if (LMODE == kLightsGlobal && kp.lnodes_lds) {
             const float4* src = reinterpret_cast<const float4*>(kp.light_nodes);
             float4* dst = reinterpret_cast<float4*>(lnodes_lds);
             for (int i = tid; i < 2 * kp.n_light_nodes; i += kBlock) dst[i] = src[i];
@@ -798,8 +815,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     LightSet<LMODE> LS;
     LS.lds = lights_lds;
     LS.glob = kp.lights;
-    LS.wl = LMODE == kLightsGlobal ? gl_lds : weights_lds;
-    LS.cl = LMODE == kLightsGlobal ? gl_lds + kp.n_lights + 1 : cdf_lds;
+    LS.wl = global_lights(LMODE) ? gl_lds : weights_lds;
+    LS.cl = global_lights(LMODE) ? gl_lds + kp.n_lights + 1 : cdf_lds;
     LS.wg = kp.weights;
     LS.cg = kp.cdf;
     if (one_light(LMODE)) {
@@ -817,15 +834,20 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     auto ltrace = [&](const LightDev& L, vec3 o, vec3 d, vec3* hp, vec3* hn) -> bool {
         if constexpr (LMODE == kLightsOneA10) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
         else if constexpr (LMODE == kLightsOneA01) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
+        else if constexpr (LMODE == kLightsGridA10) return light_trace_ax<1, 0, false>(L, o, d, hp, hn);
+        else if constexpr (LMODE == kLightsGridA01) return light_trace_ax<0, 1, false>(L, o, d, hp, hn);
         else return light_trace<LMODE == kLightsAny>(L, o, d, hp, hn);
     };
     auto lpdf = [&](const LightDev& L, vec3 o, bool h, vec3 hp, vec3 hn) -> float {
         if constexpr (LMODE == kLightsOneA10 || LMODE == kLightsOneA01) return light_pdf_ax<2, IPT_LIGHT_INR>(L, o, h, hp, hn);
+        else if constexpr (grid_lights(LMODE)) return light_pdf_ax<2, false>(L, o, h, hp, hn);
         else return light_pdf(L, o, h, hp, hn);
     };
     auto lsample = [&](const LightDev& L, vec3 o, float a, float b) -> vec3 {
         if constexpr (LMODE == kLightsOneA10) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
         else if constexpr (LMODE == kLightsOneA01) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
+        else if constexpr (LMODE == kLightsGridA10) return light_sample_dir_ax<1, 0, false>(L, o, a, b);
+        else if constexpr (LMODE == kLightsGridA01) return light_sample_dir_ax<0, 1, false>(L, o, a, b);
         else return light_sample_dir<LMODE == kLightsAny>(L, o, a, b);
     };
 
@@ -1165,7 +1187,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             int c = 0;
             if (one_light(LMODE)) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
-            } else if ((LMODE == kLightsGlobal || LMODE == kLightsAny) && kp.cdf_bsearch) {
+            } else if ((global_lights(LMODE) || LMODE == kLightsAny) && kp.cdf_bsearch) {
                 // first c with r < cdf[c] (else nl+1): the scan's answer on a
                 // non-decreasing cdf (checked at upload)
                 int hi = nl + 1;
@@ -1379,7 +1401,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (COUNT && pick < nl) ++c_lsamp;
             } else if (pick < nl) {
                 IPT_PHASE(7);
-                dir = light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1, u2);
+                dir = lsample(LS.light(pick), tpos, u1, u2);
                 if (IPT_ABL == 7)
                     keep_alive(light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
                 if (COUNT) ++c_lsamp;
@@ -1636,7 +1658,41 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             // the reference's event count: every light traced once for the
             // pdf (iterations) and once for traceRayToLight (depth < max)
             if (COUNT) c_ltr += (uint32_t)nl * ((is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u));
-            if (LMODE == kLightsGlobal && kp.n_light_nodes > 0) {
+            if constexpr (grid_lights(LMODE)) {
+                // the ray's point on the lights' plane and its cell(s): every
+                // light whose exact test can pass lies in a cell within 2^-8
+                // cells of that point (light_grid_build's lattice tolerance and
+                // the rounding of u, v are far below it), so the lights of those
+                // <= 4 cells, in index order, are the scan's hits (a light that
+                // is not hit adds +0 to lmix and is never nearest)
+                constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                const float n_dir = kp.lg_nn * comp<2>(rd);
+                const float t = div_(kp.lg_nn * (kp.lg_pn - comp<2>(ro)), n_dir);
+                const float u = (comp<XA>(ro) + comp<XA>(rd) * t - kp.lg_u0) * kp.lg_icw;
+                const float v = (comp<YA>(ro) + comp<YA>(rd) * t - kp.lg_v0) * kp.lg_ich;
+                int cand[4] = {-1, -1, -1, -1};
+                const float e = 0x1p-8f;
+                if (u > -1.0f && u < (float)kp.lg_nu + 1.0f && v > -1.0f && v < (float)kp.lg_nv + 1.0f) {
+                    const int i0 = (int)floorf(u - e), i1 = (int)floorf(u + e);
+                    const int j0 = (int)floorf(v - e), j1 = (int)floorf(v + e);
+                    const int* cells = reinterpret_cast<const int*>(lnodes_lds);
+                    auto cell = [&](int i, int j) {
+                        return (i >= 0 && i < kp.lg_nu && j >= 0 && j < kp.lg_nv) ? cells[i + kp.lg_nu * j] : -1;
+                    };
+                    cand[0] = cell(i0, j0);
+                    cand[1] = i1 != i0 ? cell(i1, j0) : -1;
+                    cand[2] = j1 != j0 ? cell(i0, j1) : -1;
+                    cand[3] = (i1 != i0 && j1 != j0) ? cell(i1, j1) : -1;
+                }
+                // ascending index order (-1 = none sorts last as 0xffffffff)
+                uint32_t c0 = (uint32_t)cand[0], c1 = (uint32_t)cand[1], c2 = (uint32_t)cand[2], c3 = (uint32_t)cand[3];
+                auto cs = [](uint32_t& a, uint32_t& b) { const uint32_t lo = a < b ? a : b; b = a < b ? b : a; a = lo; };
+                cs(c0, c1); cs(c2, c3); cs(c0, c2); cs(c1, c3); cs(c1, c2);
+                if (c0 != 0xffffffffu) light_step((int)c0);
+                if (c1 != 0xffffffffu) light_step((int)c1);
+                if (c2 != 0xffffffffu) light_step((int)c2);
+                if (c3 != 0xffffffffu) light_step((int)c3);
+            } else if (LMODE == kLightsGlobal && kp.n_light_nodes > 0) {
                 // index-ordered light BVH (ipt_bvh.h): lights met in scan order;
                 // a skipped light would add +0 to lmix and never be nearest
                 const vec3 inv = v3(safe_rcp(rd.x), safe_rcp(rd.y), safe_rcp(rd.z));
@@ -2275,8 +2331,11 @@ struct ipt_ctx {
     int cdf_bsearch = 0;
     bool any_round_light = false;
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
+    LightGrid lgrid;     // lgrid.pattern != 0: coplanar light lattice (kLightsGridA10/A01)
+    int* d_lgrid = nullptr;
     int bpc_override = 0;
     int lnodes_lds = 1;  // stage the light BVH in LDS (IPT_LNODES_LDS=0: global memory)
+    int light_grid_on = 1;  // coplanar light lattices by cell lookup (IPT_LIGHT_GRID=0: the light BVH)
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int box_inrange = 0;
     // work buffers
@@ -2452,7 +2511,9 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
                         (kp.cand_lds ? kLdsCand : 0) +
                         (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0)
-                                                : 0)) * sizeof(float);
+                                                : 0) +
+                        (grid_lights(LMODE) ? global_light_lds_words(kp.n_lights, 0) + (size_t)kp.lg_nu * kp.lg_nv
+                                            : 0)) * sizeof(float);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // persistent grid: every block the CUs can hold at once (a work queue, no
@@ -2501,6 +2562,13 @@ int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
         return launch_path3<MAXSUSP, COUNT, kLightsOne>(ctx, kp, st);
     }
     if (kp.n_lights <= kLdsLights) return launch_path3<MAXSUSP, COUNT, kLightsLds>(ctx, kp, st);
+    if constexpr (IPT_C2_ONLY == 0) {
+        // (the lattice is only built for sphere-in-box scenes)
+        if (ctx->lgrid.pattern == 1 && kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX)
+            return launch_path4<MAXSUSP, COUNT, kLightsGridA10, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+        if (ctx->lgrid.pattern == 2 && kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX)
+            return launch_path4<MAXSUSP, COUNT, kLightsGridA01, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+    }
     return launch_path3<MAXSUSP, COUNT, kLightsGlobal>(ctx, kp, st);
 }
 template <int MAXSUSP>
@@ -2594,6 +2662,15 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         // the extra LDS keeps, and gains 10 % on C5 (43.8 vs 40.2 Mpaths/s)
         kp.lnodes_lds = (ctx->lnodes_lds && ctx->n_light_nodes > 0 && ctx->n_light_nodes <= kLdsLightNodesMax) ? 1 : 0;
         kp.cdf_bsearch = ctx->cdf_bsearch;
+        kp.lgrid = ctx->d_lgrid;
+        kp.lg_nu = ctx->lgrid.nu;
+        kp.lg_nv = ctx->lgrid.nv;
+        kp.lg_u0 = ctx->lgrid.u0;
+        kp.lg_v0 = ctx->lgrid.v0;
+        kp.lg_icw = ctx->lgrid.icw;
+        kp.lg_ich = ctx->lgrid.ich;
+        kp.lg_pn = ctx->lgrid.pn;
+        kp.lg_nn = ctx->lgrid.nn;
         kp.cos_a = ctx->d_cos_a;
         kp.cos_b = ctx->d_cos_b;
         kp.frame_sc = ctx->d_frame_sc;
@@ -2690,6 +2767,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     ctx->n_cu = prop.multiProcessorCount;
     if (const char* e = std::getenv("IPT_BLOCKS_PER_CU")) ctx->bpc_override = std::atoi(e);  // profiling only
     if (const char* e = std::getenv("IPT_LNODES_LDS")) ctx->lnodes_lds = std::atoi(e) != 0;
+    if (const char* e = std::getenv("IPT_LIGHT_GRID")) ctx->light_grid_on = std::atoi(e) != 0;
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return fail(nullptr, IPT_E_DEVICE, "stream creation failed");
@@ -2709,7 +2787,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
 void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
+    void* bufs[] = {ctx->d_lgrid, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
                     ctx->d_grid_start, ctx->d_grid_items, ctx->d_frame_sc};
@@ -2810,6 +2888,10 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
             n_lnodes = 0;
         }
     }
+    LightGrid lg;
+    const bool use_lgrid = IPT_LIGHT_GRID && ctx->light_grid_on && nl > kLdsLights && !any_round &&
+                           s->geometry_kind == IPT_GEOM_SPHERE_IN_BOX && light_grid_build(L.data(), nl, lg);
+    if (!use_lgrid) lg = LightGrid{};
     bool cdf_mono = true;
     for (int i = 0; i <= nl; ++i)
         if (!(cdf[i] == cdf[i]) || (i > 0 && !(cdf[i - 1] <= cdf[i]))) cdf_mono = false;
@@ -2830,7 +2912,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         if (count) HIPCHECK(ctx, hipMemcpy(buf.p, src, sizeof(T) * count, hipMemcpyHostToDevice));
         return IPT_OK;
     };
-    DevBuf<int> n_grid_start;
+    DevBuf<int> n_grid_start, n_lgrid;
     DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
     DevBuf<BvhNode> n_light_nodes, n_bvh_nodes;
     DevBuf<LightDev> n_lights;
@@ -2841,6 +2923,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
     if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
     if (!lnodes.empty() && !rc) rc = upload(n_light_nodes, lnodes.data(), lnodes.size());
+    if (use_lgrid && !rc) rc = upload(n_lgrid, lg.cells.data(), lg.cells.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_nodes, bnodes.data(), bnodes.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_prims, bprims.data(), bprims.size());
     if (!rc) rc = upload(n_lights, L.data(), L.size());
@@ -2850,7 +2933,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!rc) rc = upload(n_spheres, sph.data(), sph.size());
     if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
-                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_wall};
+                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_wall, ctx->d_lgrid};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_grid_start = n_grid_start.release();
@@ -2865,6 +2948,9 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     }
     ctx->d_light_nodes = n_light_nodes.release();
     ctx->n_light_nodes = lnodes.empty() ? 0 : n_lnodes;
+    ctx->d_lgrid = n_lgrid.release();
+    lg.cells.clear();
+    ctx->lgrid = lg;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
     ctx->any_round_light = any_round;
     // the axis-aligned single-light instances also take the range-free roots

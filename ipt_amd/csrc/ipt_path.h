@@ -8,6 +8,8 @@
 
 #include "ipt_math.h"
 
+#include <vector>
+
 namespace ipt {
 
 constexpr int kMaxLights = 1024;
@@ -627,6 +629,83 @@ inline bool light_ranges_box(const LightDev& L, int na, const float cam[3]) {
     const float pn = P[na];
     return dmin >= 0x1p-8 && dmax <= 0x1p8 && L.area >= 0x1p-16f && L.area <= 0x1p16f &&
            __builtin_fabs(n[na]) >= 0x1p-16f && __builtin_fabs(n[na]) <= 0x1p16f && __builtin_fabs(pn) >= 0x1p-8f;
+}
+
+// Coplanar light lattice (kLightsGridA10/A01, the many-light C5 scene's 16 x 16
+// emitters): every light an axis-aligned diamond AreaLight with the same axis
+// pattern, the same normal and the same plane coordinate P[2] (so every
+// light's traceRay computes the same t and plane point q), and its rectangle
+// in the plane's (u, v) = (q[XA], q[YA]) one cell of a uniform lattice (within
+// 2^-12 of a cell on each edge), at most one light per cell. A light's exact
+// test passes only for q inside its rectangle up to a relative 2^-21, and the
+// kernel's cell coordinates of q are off by < 2^-13 cells for |u|, |v| <= 257,
+// so the lights of the cells within 2^-8 of (u, v) contain every hit.
+struct LightGrid {
+    int pattern = 0;  // axis_aligned_light() of every light; 0 = no lattice
+    int nu = 0, nv = 0;
+    float u0 = 0.0f, v0 = 0.0f, icw = 0.0f, ich = 0.0f, pn = 0.0f, nn = 0.0f;
+    std::vector<int> cells;  // [nv][nu] light index, -1 = empty
+};
+inline bool light_grid_build(const LightDev* L, int nl, LightGrid& g) {
+    if (nl < 2) return false;
+    const int pat = axis_aligned_light(L[0]);
+    if (pat == 0) return false;
+    const int XA = pat == 1 ? 1 : 0, YA = 1 - XA;
+    auto c = [](vec3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); };
+    std::vector<double> lu(nl), hu(nl), lv(nl), hv(nl);
+    for (int i = 0; i < nl; ++i) {
+        if (L[i].type != 0 || axis_aligned_light(L[i]) != pat) return false;
+        if (f2u(L[i].n.z) != f2u(L[0].n.z) || f2u(L[i].P.z) != f2u(L[0].P.z)) return false;
+        const double pu = c(L[i].P, XA), xu = c(L[i].x, XA), pv = c(L[i].P, YA), yv = c(L[i].y, YA);
+        lu[i] = pu + (xu < 0.0 ? xu : 0.0);
+        hu[i] = pu + (xu > 0.0 ? xu : 0.0);
+        lv[i] = pv + (yv < 0.0 ? yv : 0.0);
+        hv[i] = pv + (yv > 0.0 ? yv : 0.0);
+    }
+    const double cw = hu[0] - lu[0], ch = hv[0] - lv[0];
+    if (!(cw >= 0x1p-20 && ch >= 0x1p-20)) return false;
+    double u0 = lu[0], v0 = lv[0];
+    for (int i = 1; i < nl; ++i) {
+        u0 = lu[i] < u0 ? lu[i] : u0;
+        v0 = lv[i] < v0 ? lv[i] : v0;
+    }
+    const double tol = 0x1p-12;
+    std::vector<int> ci(nl), cj(nl);
+    int nu = 0, nv = 0;
+    for (int i = 0; i < nl; ++i) {
+        const double fi = (lu[i] - u0) / cw, fj = (lv[i] - v0) / ch;
+        const double ri = __builtin_floor(fi + 0.5), rj = __builtin_floor(fj + 0.5);
+        if (!(__builtin_fabs(fi - ri) <= tol && __builtin_fabs((hu[i] - u0) / cw - (ri + 1.0)) <= tol &&
+              __builtin_fabs(fj - rj) <= tol && __builtin_fabs((hv[i] - v0) / ch - (rj + 1.0)) <= tol))
+            return false;
+        if (ri < 0.0 || rj < 0.0 || ri >= 256.0 || rj >= 256.0) return false;
+        ci[i] = (int)ri;
+        cj[i] = (int)rj;
+        nu = ci[i] + 1 > nu ? ci[i] + 1 : nu;
+        nv = cj[i] + 1 > nv ? cj[i] + 1 : nv;
+    }
+    if (nu * nv > 4096) return false;
+    const double umax = u0 + nu * cw, vmax = v0 + nv * ch;
+    if (!(__builtin_fabs(u0) <= 0x1p20 && __builtin_fabs(umax) <= 0x1p20 && __builtin_fabs(v0) <= 0x1p20 &&
+          __builtin_fabs(vmax) <= 0x1p20 && cw >= 0x1p-12 * (__builtin_fabs(u0) + __builtin_fabs(umax)) &&
+          ch >= 0x1p-12 * (__builtin_fabs(v0) + __builtin_fabs(vmax))))
+        return false;  // cells small against their coordinates: rounding could exceed the margin
+    g.cells.assign((size_t)nu * nv, -1);
+    for (int i = 0; i < nl; ++i) {
+        int& cell = g.cells[(size_t)ci[i] + (size_t)nu * cj[i]];
+        if (cell >= 0) return false;  // two lights in one cell
+        cell = i;
+    }
+    g.pattern = pat;
+    g.nu = nu;
+    g.nv = nv;
+    g.u0 = (float)u0;
+    g.v0 = (float)v0;
+    g.icw = (float)(1.0 / cw);
+    g.ich = (float)(1.0 / ch);
+    g.pn = L[0].P.z;
+    g.nn = L[0].n.z;
+    return true;
 }
 
 // Light constructor derived fields: AreaLight (lighting.cpp:79-90) + the

@@ -192,18 +192,73 @@ def test_random_lights_bit_exact(gpu_ctx, oracle, n):
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
 
 
-def test_light_bvh_active(gpu_ctx):
-    """The 256-emitter scene runs the light BVH: far fewer light tests than
-    the reference's L traces per ray, and the reference event count intact."""
-    gpu_ctx.upload_scene(scenes.make_scene_box_lights(16))
+def _light_counters(ctx, desc):
+    ctx.upload_scene(desc)
     p = capi.make_params(32, 32, 1, n_rays=16, depth_max=8, flags=capi.IPT_FLAG_COUNTERS)
     img = {"pixels": np.zeros(32 * 32, np.float32), "counters": np.zeros(32 * 32, np.uint32)}
-    gpu_ctx.reset_counters()
-    gpu_ctx.render(p, img)
-    c = gpu_ctx.counters()
+    ctx.reset_counters()
+    ctx.render(p, img)
+    return ctx.counters()
+
+
+def test_light_bvh_active(monkeypatch):
+    """With the lattice lookup off (IPT_LIGHT_GRID=0) the 256-emitter scene runs
+    the light BVH: far fewer light tests than the reference's L traces per ray,
+    and the reference event count intact."""
+    monkeypatch.setenv("IPT_LIGHT_GRID", "0")
+    ctx = capi.Context(0)
+    try:
+        c = _light_counters(ctx, scenes.make_scene_box_lights(16))
+    finally:
+        ctx.close()
     assert c["light_nodes"] > 0
     assert c["light_tests"] < 0.1 * 256 * c["traced_rays"]
     assert c["light_traces"] >= 256 * c["traced_rays"]
+
+
+def test_light_grid_active(gpu_ctx):
+    """The 256 co-planar emitters lie on a lattice: each ray tests the lights of
+    the one to four cells around its plane point (no BVH nodes), and the
+    reference event count stays intact."""
+    c = _light_counters(gpu_ctx, scenes.make_scene_box_lights(16))
+    assert c["light_nodes"] == 0
+    assert 0 < c["light_tests"] < 1.2 * c["traced_rays"]
+    assert c["light_traces"] >= 256 * c["traced_rays"]
+
+
+@pytest.mark.parametrize("k", [5, 8, 16, 32])
+def test_light_grid_bit_exact(gpu_ctx, oracle, k):
+    """kLightsGridA10: the lattice lookup finds every light the full scan hits
+    (k x k emitters, 25 to 1 024 lights) -- bit-exact vs the oracle, with more
+    samples per pixel so that many plane points fall within the lookup's
+    margin of a cell edge."""
+    desc = scenes.make_scene_box_lights(k)
+    p = capi.make_params(32, 24, 4, n_rays=8, depth_max=6)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+@pytest.mark.parametrize("variant", ["nudged", "gap", "mixed_axes"])
+def test_light_grid_fallback_bit_exact(gpu_ctx, oracle, variant):
+    """Light sets that are not a lattice (one emitter moved by a tenth of a
+    cell, one emitter with swapped axes) take the light BVH; a lattice with an
+    empty row keeps the cell lookup (empty cells): all bit-exact."""
+    desc = scenes.make_scene_box_lights(8)
+    L = [dict(l) for l in desc["lights"]]
+    if variant == "nudged":
+        c = list(L[9]["position"])
+        c[1] = float(np.float32(c[1] + np.float32(0.0025)))
+        L[9]["position"] = c
+    elif variant == "gap":
+        L = L[:8] + L[16:]
+    else:
+        L[3]["x_axis"], L[3]["y_axis"] = L[3]["y_axis"], L[3]["x_axis"]
+    desc = dict(desc, lights=L)
+    p = capi.make_params(24, 20, 2, n_rays=8, depth_max=6)
+    gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
+    assert np.array_equal(gc, oc)
+    assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
 
 
 @pytest.mark.parametrize("name", ["make_scene_square_lit_by_square", "make_scene_lit_corner"])
@@ -292,6 +347,7 @@ def test_light_bvh_in_lds_bit_exact(oracle, monkeypatch, desc_fn, lds):
     (IPT_LNODES_LDS=0, read at ipt_create) walk the same nodes: bit-exact vs
     the oracle."""
     monkeypatch.setenv("IPT_LNODES_LDS", lds)
+    monkeypatch.setenv("IPT_LIGHT_GRID", "0")  # the lattice scene would not walk the BVH
     ctx = capi.Context(0)
     try:
         desc = desc_fn()
