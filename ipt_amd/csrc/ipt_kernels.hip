@@ -193,6 +193,7 @@ struct KParams {
     float lg_u0, lg_v0, lg_icw, lg_ich;   // cell coordinates: (q - u0) * icw
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
+    const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
     int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
@@ -238,6 +239,9 @@ struct KParams {
 #endif
 #ifndef IPT_LIGHT_GRID
 #define IPT_LIGHT_GRID 1  // coplanar light lattices by cell lookup (kLightsGridA10/A01)
+#endif
+#ifndef IPT_CDF_LO
+#define IPT_CDF_LO 1  // many lights: the pick's scan started from a 256-bucket table
 #endif
 #ifndef IPT_RAYGEN
 #define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
@@ -622,8 +626,12 @@ __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
 // from L2 by the CosineDdf gathers, and the pick / walk are chains of
 // dependent loads.
 constexpr int kLdsLightNodesMax = 512;
+// [weights | cdf | cdf bucket starts (kCdfBuckets)] then the light BVH nodes or
+// the lattice cells, 16-byte aligned
+constexpr int kCdfBuckets = 256;
+__host__ __device__ inline int global_light_prefix_words(int nl) { return (2 * (nl + 1) + kCdfBuckets + 3) & ~3; }
 __host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds) {
-    return (size_t)((2 * (nl + 1) + 3) & ~3) + 8 * (size_t)n_nodes_lds;
+    return (size_t)global_light_prefix_words(nl) + 8 * (size_t)n_nodes_lds;
 }
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4
@@ -781,7 +789,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                                            // [kLdsCand] when kp.cand_lds
     // kLightsGlobal: [weights | cdf | light BVH nodes] after the candidate rows
     float* gl_lds = reinterpret_cast<float*>(cand_lds) + (kp.cand_lds ? kLdsCand : 0);
-    BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + ((2 * (kp.n_lights + 1) + 3) & ~3));
+    BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + global_light_prefix_words(kp.n_lights));
+    int* cdf_lo_lds = reinterpret_cast<int*>(gl_lds + 2 * (kp.n_lights + 1));
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
@@ -803,6 +812,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             gl_lds[i] = kp.weights[i];
             gl_lds[kp.n_lights + 1 + i] = kp.cdf[i];
         }
+        if (kp.cdf_lo)
+            for (int i = tid; i < kCdfBuckets; i += kBlock) cdf_lo_lds[i] = kp.cdf_lo[i];
         if (grid_lights(LMODE))
             for (int i = tid; i < kp.lg_nu * kp.lg_nv; i += kBlock) reinterpret_cast<int*>(lnodes_lds)[i] = kp.lgrid[i];
         if (LMODE == kLightsGlobal && kp.lnodes_lds) {
@@ -834,20 +845,20 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     auto ltrace = [&](const LightDev& L, vec3 o, vec3 d, vec3* hp, vec3* hn) -> bool {
         if constexpr (LMODE == kLightsOneA10) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
         else if constexpr (LMODE == kLightsOneA01) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
-        else if constexpr (LMODE == kLightsGridA10) return light_trace_ax<1, 0, false>(L, o, d, hp, hn);
-        else if constexpr (LMODE == kLightsGridA01) return light_trace_ax<0, 1, false>(L, o, d, hp, hn);
+        else if constexpr (LMODE == kLightsGridA10) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
+        else if constexpr (LMODE == kLightsGridA01) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
         else return light_trace<LMODE == kLightsAny>(L, o, d, hp, hn);
     };
     auto lpdf = [&](const LightDev& L, vec3 o, bool h, vec3 hp, vec3 hn) -> float {
         if constexpr (LMODE == kLightsOneA10 || LMODE == kLightsOneA01) return light_pdf_ax<2, IPT_LIGHT_INR>(L, o, h, hp, hn);
-        else if constexpr (grid_lights(LMODE)) return light_pdf_ax<2, false>(L, o, h, hp, hn);
+        else if constexpr (grid_lights(LMODE)) return light_pdf_ax<2, IPT_LIGHT_INR>(L, o, h, hp, hn);
         else return light_pdf(L, o, h, hp, hn);
     };
     auto lsample = [&](const LightDev& L, vec3 o, float a, float b) -> vec3 {
         if constexpr (LMODE == kLightsOneA10) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
         else if constexpr (LMODE == kLightsOneA01) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
-        else if constexpr (LMODE == kLightsGridA10) return light_sample_dir_ax<1, 0, false>(L, o, a, b);
-        else if constexpr (LMODE == kLightsGridA01) return light_sample_dir_ax<0, 1, false>(L, o, a, b);
+        else if constexpr (LMODE == kLightsGridA10) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
+        else if constexpr (LMODE == kLightsGridA01) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
         else return light_sample_dir<LMODE == kLightsAny>(L, o, a, b);
     };
 
@@ -1187,6 +1198,13 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             int c = 0;
             if (one_light(LMODE)) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+            } else if (global_lights(LMODE) && kp.cdf_lo) {
+                // the scan from the first index whose cdf exceeds r's bucket
+                // start floor(256 r)/256 (host table): every earlier entry is
+                // <= that start <= r, so the scan would pass it; a bucket holds
+                // at most 8 entries (else the table is not built)
+                c = cdf_lo_lds[(int)(r * 256.0f)];
+                while (c <= nl && !(r < LS.cdf(c))) ++c;
             } else if ((global_lights(LMODE) || LMODE == kLightsAny) && kp.cdf_bsearch) {
                 // first c with r < cdf[c] (else nl+1): the scan's answer on a
                 // non-decreasing cdf (checked at upload)
@@ -1383,7 +1401,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // one is selected (a mixed wave runs both anyway), so the CosineDdf
         // gathers have an unconditional consumer and stay unconditional loads
         vec3 dir_bf = v3(0, 0, 0);
-        if constexpr (one_light(LMODE)) {
+        // (the lattice instances measured 3 % slower this way: their light sample
+        // reads the picked light's record, and both directions cost more there)
+        constexpr bool kDirBf = one_light(LMODE);
+        if constexpr (kDirBf) {
             Frame fm;
             fm.m0 = v3(frc[0 * kFrameStride], frc[1 * kFrameStride], frc[2 * kFrameStride]);
             fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
@@ -1396,7 +1417,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }
         if (iter_lane) {
             vec3 dir = v3(0, 0, 0);
-            if (one_light(LMODE)) {
+            if (kDirBf) {
                 dir = dir_bf;
                 if (COUNT && pick < nl) ++c_lsamp;
             } else if (pick < nl) {
@@ -2329,6 +2350,7 @@ struct ipt_ctx {
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
+    int* d_cdf_lo = nullptr;  // cdf bucket starts (global light modes), null when a bucket is crowded
     bool any_round_light = false;
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
     LightGrid lgrid;     // lgrid.pattern != 0: coplanar light lattice (kLightsGridA10/A01)
@@ -2662,6 +2684,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         // the extra LDS keeps, and gains 10 % on C5 (43.8 vs 40.2 Mpaths/s)
         kp.lnodes_lds = (ctx->lnodes_lds && ctx->n_light_nodes > 0 && ctx->n_light_nodes <= kLdsLightNodesMax) ? 1 : 0;
         kp.cdf_bsearch = ctx->cdf_bsearch;
+        kp.cdf_lo = ctx->d_cdf_lo;
         kp.lgrid = ctx->d_lgrid;
         kp.lg_nu = ctx->lgrid.nu;
         kp.lg_nv = ctx->lgrid.nv;
@@ -2787,7 +2810,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
 void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_lgrid, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
+    void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
                     ctx->d_grid_start, ctx->d_grid_items, ctx->d_frame_sc};
@@ -2891,7 +2914,26 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     LightGrid lg;
     const bool use_lgrid = IPT_LIGHT_GRID && ctx->light_grid_on && nl > kLdsLights && !any_round &&
                            s->geometry_kind == IPT_GEOM_SPHERE_IN_BOX && light_grid_build(L.data(), nl, lg);
-    if (!use_lgrid) lg = LightGrid{};
+    // (the lattice instances take the range-free light arithmetic: every
+    // light's ranges proven as for the single light)
+    bool lg_inr = use_lgrid;
+    for (int i = 0; lg_inr && i < nl; ++i) lg_inr = light_ranges_box(L[i], 2, cam);
+    if (!use_lgrid || !lg_inr) lg = LightGrid{};
+    // bucket starts of the pick's scan: lo[b] = first c with cdf[c] > b/256
+    // (the float compare the scan makes; nl+1 if none); kept when no bucket
+    // spans more than 8 entries
+    std::vector<int> cdf_lo(kCdfBuckets);
+    bool use_cdf_lo = IPT_CDF_LO && nl > kLdsLights && !any_round;
+    for (int b = 0; use_cdf_lo && b < kCdfBuckets; ++b) {
+        const float start = (float)b / (float)kCdfBuckets;
+        int c = 0;
+        while (c <= nl && !(start < cdf[c])) ++c;
+        cdf_lo[b] = c;
+        const float end = (float)(b + 1) / (float)kCdfBuckets;
+        int e = c;
+        while (e <= nl && !(end < cdf[e])) ++e;
+        if (e - c > 8) use_cdf_lo = false;
+    }
     bool cdf_mono = true;
     for (int i = 0; i <= nl; ++i)
         if (!(cdf[i] == cdf[i]) || (i > 0 && !(cdf[i - 1] <= cdf[i]))) cdf_mono = false;
@@ -2912,7 +2954,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         if (count) HIPCHECK(ctx, hipMemcpy(buf.p, src, sizeof(T) * count, hipMemcpyHostToDevice));
         return IPT_OK;
     };
-    DevBuf<int> n_grid_start, n_lgrid;
+    DevBuf<int> n_grid_start, n_lgrid, n_cdf_lo;
     DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
     DevBuf<BvhNode> n_light_nodes, n_bvh_nodes;
     DevBuf<LightDev> n_lights;
@@ -2923,7 +2965,8 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
     if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
     if (!lnodes.empty() && !rc) rc = upload(n_light_nodes, lnodes.data(), lnodes.size());
-    if (use_lgrid && !rc) rc = upload(n_lgrid, lg.cells.data(), lg.cells.size());
+    if (lg.pattern && !rc) rc = upload(n_lgrid, lg.cells.data(), lg.cells.size());
+    if (use_cdf_lo && !rc) rc = upload(n_cdf_lo, cdf_lo.data(), cdf_lo.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_nodes, bnodes.data(), bnodes.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_prims, bprims.data(), bprims.size());
     if (!rc) rc = upload(n_lights, L.data(), L.size());
@@ -2933,7 +2976,8 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!rc) rc = upload(n_spheres, sph.data(), sph.size());
     if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
-                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_wall, ctx->d_lgrid};
+                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_wall, ctx->d_lgrid,
+                   ctx->d_cdf_lo};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_grid_start = n_grid_start.release();
@@ -2949,6 +2993,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->d_light_nodes = n_light_nodes.release();
     ctx->n_light_nodes = lnodes.empty() ? 0 : n_lnodes;
     ctx->d_lgrid = n_lgrid.release();
+    ctx->d_cdf_lo = n_cdf_lo.release();
     lg.cells.clear();
     ctx->lgrid = lg;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
