@@ -629,9 +629,13 @@ constexpr int kLdsLightNodesMax = 512;
 // [weights | cdf | cdf bucket starts (kCdfBuckets)] then the light BVH nodes or
 // the lattice cells, 16-byte aligned
 constexpr int kCdfBuckets = 256;
-__host__ __device__ inline int global_light_prefix_words(int nl) { return (2 * (nl + 1) + kCdfBuckets + 3) & ~3; }
-__host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds) {
-    return (size_t)global_light_prefix_words(nl) + 8 * (size_t)n_nodes_lds;
+// The lattice instances leave the weights in global memory (read once per hit
+// light) so that C5's 256 emitters fit 4 workgroups per CU: [cdf | buckets].
+__host__ __device__ inline int global_light_prefix_words(int nl, bool grid = false) {
+    return ((grid ? 1 : 2) * (nl + 1) + kCdfBuckets + 3) & ~3;
+}
+__host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds, bool grid = false) {
+    return (size_t)global_light_prefix_words(nl, grid) + 8 * (size_t)n_nodes_lds;
 }
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4
@@ -672,6 +676,7 @@ struct LightSet {
     }
     __device__ __forceinline__ float weight(int i) const {
         if (one_light(LMODE)) return w0;
+        if (grid_lights(LMODE)) return wg[i];
         if (LMODE == kLightsLds || global_lights(LMODE)) return wl[i];
         return wg[i];
     }
@@ -789,8 +794,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                                            // [kLdsCand] when kp.cand_lds
     // kLightsGlobal: [weights | cdf | light BVH nodes] after the candidate rows
     float* gl_lds = reinterpret_cast<float*>(cand_lds) + (kp.cand_lds ? kLdsCand : 0);
-    BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + global_light_prefix_words(kp.n_lights));
-    int* cdf_lo_lds = reinterpret_cast<int*>(gl_lds + 2 * (kp.n_lights + 1));
+    constexpr bool kGridL = grid_lights(LMODE);
+    BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + global_light_prefix_words(kp.n_lights, kGridL));
+    float* cdf_gl = gl_lds + (kGridL ? 0 : kp.n_lights + 1);
+    int* cdf_lo_lds = reinterpret_cast<int*>(cdf_gl + kp.n_lights + 1);
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
@@ -809,8 +816,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         for (int i = tid; i < kp.n_cand; i += kBlock) cand_lds[i] = kp.cand_rows[i];
     if (global_lights(LMODE)) {
         for (int i = tid; i <= kp.n_lights; i += kBlock) {
-            gl_lds[i] = kp.weights[i];
-            gl_lds[kp.n_lights + 1 + i] = kp.cdf[i];
+            if (!kGridL) gl_lds[i] = kp.weights[i];
+            cdf_gl[i] = kp.cdf[i];
         }
         if (kp.cdf_lo)
             for (int i = tid; i < kCdfBuckets; i += kBlock) cdf_lo_lds[i] = kp.cdf_lo[i];
@@ -827,7 +834,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     LS.lds = lights_lds;
     LS.glob = kp.lights;
     LS.wl = global_lights(LMODE) ? gl_lds : weights_lds;
-    LS.cl = global_lights(LMODE) ? gl_lds + kp.n_lights + 1 : cdf_lds;
+    LS.cl = global_lights(LMODE) ? cdf_gl : cdf_lds;
     LS.wg = kp.weights;
     LS.cg = kp.cdf;
     if (one_light(LMODE)) {
@@ -2534,7 +2541,7 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
                         (kp.cand_lds ? kLdsCand : 0) +
                         (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0)
                                                 : 0) +
-                        (grid_lights(LMODE) ? global_light_lds_words(kp.n_lights, 0) + (size_t)kp.lg_nu * kp.lg_nv
+                        (grid_lights(LMODE) ? global_light_lds_words(kp.n_lights, 0, true) + (size_t)kp.lg_nu * kp.lg_nv
                                             : 0)) * sizeof(float);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
