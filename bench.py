@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[1]): sample_scenes[0] (make_scene_box), 1024^2,
 256 spp, n_rays 16, depth_max 8, fp32, synthetic = the scene itself.
 A *step* renders `--spp-per-step` sample passes of the whole frame (one
-ipt_render_device call: path kernel + GridRenderPlane accumulate kernel); the
-default 8 steps x 32 spp is the full 256-spp frame.
+ipt_render_device call: raygen + path kernel + GridRenderPlane accumulate
+kernel); the default step is the full 256-spp frame, rendered by one
+path-kernel launch.
 
 Multi-GPU (torchrun, one rank per GPU): the frame's destination rows are cut
 into 16-row tiles dealt round-robin to the ranks (weak scaling: the frame is
@@ -30,12 +31,17 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 
-# BASELINE.json configs: (scene, width, per-rank height, spp per step, steps)
+# BASELINE.json configs: (scene, width, per-rank height, spp per step, steps).
+# A step is one ipt_render_device call: c2's step is the whole 1024^2 x 256 spp
+# frame (one launch of 268 M paths); c3/c5 sample their full spp counts with
+# calls of 16.8 M / 134 M paths. The persistent kernel's end-of-launch tail
+# (lanes out of work while the longest paths finish) is then a small share of
+# the launch, as in the full job.
 CONFIGS = {
-    "c2": ("box", 1024, 1024, 32, 8),       # configs[1]: 1024^2, 256 spp, 8 bounces (the metric)
-    "c3": ("spheres10k", 1024, 1024, 1, 4),  # configs[2]: 10k spheres (64 spp in full; sampled)
+    "c2": ("box", 1024, 1024, 256, 2),      # configs[1]: 1024^2, 256 spp, 8 bounces (the metric)
+    "c3": ("spheres10k", 1024, 1024, 16, 2),  # configs[2]: 10k spheres (64 spp in full; sampled)
     "c4": ("box", 4096, 4096, 8, 4),         # configs[3]: 4096^2 tiles across GPUs (1024 spp in full)
-    "c5": ("lights256", 2048, 2048, 2, 4),   # configs[4]: 256 emitters, 2048^2 (512 spp in full)
+    "c5": ("lights256", 2048, 2048, 32, 2),  # configs[4]: 256 emitters, 2048^2 (512 spp in full)
 }
 
 

@@ -2613,10 +2613,15 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     const int W = p->width, H = p->height;
     const size_t per_pass = (size_t)n_cand * W;
     if (per_pass == 0 || p->spp == 0) return IPT_OK;
-    // chunk passes so that the work buffers stay bounded: 2^27 units = 512 MiB
-    // of radiance + 128 MiB of codes + 4 GiB of raygen records
-    const size_t budget = (size_t)1 << 27;
-    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)p->spp, budget / per_pass));
+    // chunk passes so that the work buffers stay bounded: 2^29 units = 2 GiB of
+    // radiance + 512 MiB of codes + 16 GiB of raygen records (of 288 GB), in
+    // equal chunks: each launch ends with a tail in which lanes run out of work
+    // (the longest paths finish alone; 7 % of a 32-spp C2 launch), so few large
+    // launches beat many small ones (C2 1024^2 x 256 spp is a single launch)
+    const size_t budget = (size_t)1 << 29;
+    const size_t n_chunks = std::max<size_t>(1, ((size_t)p->spp * per_pass + budget - 1) / budget);
+    int chunk = (int)std::max<size_t>(1, ((size_t)p->spp + n_chunks - 1) / n_chunks);
+    while (chunk > 1 && (size_t)chunk * per_pass > budget) --chunk;
     if (host_values) chunk = p->spp;  // debug path: one chunk
     int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
     if (rc) return rc;
