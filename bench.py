@@ -244,7 +244,8 @@ def main():
             ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64, device=dev)
             coll(dist.all_reduce, ct)
             cnt = dict(zip(capi.COUNTER_NAMES, [int(x) for x in ct.tolist()]))
-        ops = roofline.ops_from_counters(cnt, n_spheres=len(desc.get("spheres", [])))
+        ops = roofline.ops_from_counters(cnt, n_spheres=len(desc.get("spheres", [])),
+                                         n_lights=len(desc.get("lights", [])))
         # per launch on one rank: ops/world per launch, average launch duration
         launch_s = path_ms / 1e3 / args.steps
         achieved = ops / world / args.steps / launch_s
@@ -299,7 +300,9 @@ def main():
             # the reference's full sphere/light scans, only where a BVH replaced them
             "reference_scan_ops_per_path": (roofline.reference_scan_ops(cnt, len(desc.get("spheres", [])))
                                             / cnt["paths"]
-                                            if cnt["bvh_nodes"] or cnt["light_nodes"] else None),
+                                            if cnt["bvh_nodes"] or cnt["light_nodes"]
+                                            or roofline.light_lattice(cnt, len(desc.get("lights", [])))
+                                            else None),
             "note": ("hbm: algorithmic bytes of one path launch (5 B radiance + drift code and "
                      "the 32 B raygen record per path, 4 B CosineDdf r gather per cosine-sampled "
                      "iteration, 8 B frame-table gather per sphere frame) / HIP-event launch "

@@ -1,9 +1,9 @@
 """Algorithmic cost model of the hot path and gfx950 peaks.
 
-The path kernel is bound by instruction issue and the latency of its random
-table gathers (no MFMA; its HBM traffic is the radiance output, the raygen
-records and the CosineDdf / frame-table gathers: ~0.6 KB per path at a
-fraction of 8 TB/s), so its roofline is the VALU issue rate. The op count
+The path kernel is bound by instruction issue (no MFMA; its HBM traffic is
+the radiance output, the raygen records and the CosineDdf / frame-table
+gathers: ~0.6 KB per path at a fraction of 8 TB/s, their latency hidden), so
+its roofline is the VALU issue rate. The op count
 is ALGORITHMIC: the reference's own arithmetic per event, counted as written
 (no credit for work the GPU kernel avoids, e.g. precomputed wall frames), with
 each transcendental (acos, sin, cos) at 20 op-eq. Event counts come from the
@@ -34,21 +34,33 @@ OPS = {
     "node_finalize": 1,
     "sphere_test": 37,       # intersection_with_sphere + FractalSpheres acceptance
     "bvh_node": 29,          # slab test + entry/prune compares, per BVH node visited
+    "light_cell": 30,        # light lattice: plane point, cell coordinates, <= 4 cell reads, per trace
 }
 TRANSC = {"rotate_build": 3, "iter_cosine": 4}
 
 
-def ops_from_counters(c: dict, n_spheres: int = 0) -> float:
+def light_lattice(c: dict, n_lights: int) -> bool:
+    """The many-light scene ran the light lattice lookup (no BVH nodes, and far
+    fewer light tests than the reference's scans)."""
+    return (n_lights > 16 and c.get("light_nodes", 0) == 0
+            and c["light_tests"] < 0.25 * max(c["light_traces"], 1))
+
+
+def ops_from_counters(c: dict, n_spheres: int = 0, n_lights: int = 1) -> float:
     """Algorithmic op-eq for a set of ipt_counters. The base formula is §8(d)'s
     for sample_scenes[0]; many-light scenes add 57 per AreaLight::traceRay
     beyond the box's two per traced ray, sphere-stress scenes add 37 per
-    sphere test (§8(d): "C3 adds N x 37 per trace")."""
+    sphere test (§8(d): "C3 adds N x 37 per trace"). Where a BVH or the light
+    lattice replaced a scan, the tests actually run are priced (plus 29 per
+    BVH node, 30 per lattice lookup), not the scan."""
     kept_light = c["light_samples"] - c["skipped"]
     cosine = c["iterations"] - c["light_samples"]
-    light_bvh = c.get("light_nodes", 0) > 0
+    lattice = light_lattice(c, n_lights)
+    light_bvh = c.get("light_nodes", 0) > 0 or lattice
     f = (c["paths"] * OPS["camera"]
          + c["traced_rays"] * OPS["geom_trace"]
-         + (c["light_tests"] * OPS["light_trace"] + c["light_nodes"] * OPS["bvh_node"] if light_bvh
+         + (c["light_tests"] * OPS["light_trace"] + c["light_nodes"] * OPS["bvh_node"]
+            + (c["traced_rays"] * OPS["light_cell"] if lattice else 0) if light_bvh
             else c["traced_rays"] * OPS["light_trace"])
          + c["light_hits"] * OPS["occlusion"]
          + c["surface_hits"] * (OPS["rotate_build"] + TRANSC["rotate_build"] * TRANSC_OP_EQ)
