@@ -293,6 +293,9 @@ constexpr size_t kFrameTabEntries = 2 * ((size_t)kFrameTabSpan + 1);
 #ifndef IPT_FRAME_TAB
 #define IPT_FRAME_TAB 1  // +8.6 % C2
 #endif
+#ifndef IPT_FRAME_FAST_ALL
+#define IPT_FRAME_FAST_ALL 1  // the fast frame build for the sphere-list scenes too
+#endif
 #ifndef IPT_FRAME_FAST
 #define IPT_FRAME_FAST 1  // sphere-in-box frames without glm's zero terms (make_frame_sc_fast)
 #endif
@@ -1323,10 +1326,21 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     } else {
                         f = make_frame_sc<kFrameInrange>(to, fs, fc);
                     }
-                } else if (kFrameInrange)
+                } else if (kFrameInrange) {
                     f = make_frame<true>(normalize_inrange_(nrm));
-                else
+                } else if (IPT_FRAME_FAST_ALL) {
+                    // sphere-list scenes: the f64 angle, then the fast build
+                    // (its own range checks; a normalized `to`), exact fallback
+                    const vec3 to = normalize(nrm);
+                    float fs, fc;
+                    frame_angle_sc(to, &fs, &fc);
+                    bool ok;
+                    f = make_frame_sc_fast(to, fs, fc, ok);
+                    if (__builtin_expect(__any(!ok), 0))
+                        if (!ok) f = make_frame_sc<false>(to, fs, fc);
+                } else {
                     f = make_frame(normalize(nrm));
+                }
             }
             if (IPT_ABL == 1) keep_alive(make_frame(normalize(nrm * (1.0f + kp.abl_zero))));
             float* c = lfr + tid;
