@@ -173,7 +173,14 @@ const char* ipt_last_error(ipt_ctx* ctx); /* ctx may be NULL (creation errors) *
 
 /* A context owns its stream and device buffers. The first render allocates its
  * exact sampling tables once: CosineDdf 192 MiB and, for sphere-in-box scenes,
- * the RotateDdf frame-angle table 1 GiB (freed by ipt_destroy). */
+ * the RotateDdf frame-angle table 1 GiB (freed by ipt_destroy). Work buffers
+ * grow to the largest render: 37 B per sample (radiance, drift code, raygen
+ * record) in chunks of at most 2^29 samples; a call renders all its passes in
+ * as few path-kernel launches as that allows (each launch ends in a tail
+ * where lanes have run out of paths, so batch passes per call).
+ * Environment read here (diagnostics): IPT_LNODES_LDS=0 keeps the light BVH in
+ * global memory, IPT_LIGHT_GRID=0 disables the light-lattice lookup (the light
+ * BVH is used instead), IPT_BLOCKS_PER_CU caps the path kernel's residency. */
 int ipt_create(int hip_device, ipt_ctx** out);
 void ipt_destroy(ipt_ctx* ctx);
 
