@@ -356,6 +356,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
+            # geometry traces per second beside the paths
+            "mrays_per_s": (value * cnt["traced_rays"] / cnt["paths"]) if cnt else None,
             "events_per_path": ({k: cnt[k] / cnt["paths"] for k in cnt if k != "paths"}
                                 if cnt else None),
             "mean_pixel": float(pixels.mean().item()),
