@@ -848,6 +848,40 @@ double ipt_oracle_render_rows(const ipt_scene* scene, const ipt_params* p, int r
     if (paths) *paths = (uint64_t)nrows * (uint64_t)W;
     return total;
 }
+
+// Full-size parity (tests/test_gpu_parity.py): the clamped root values of the
+// source pixels (ix, iy) with iy = row_phase (mod row_step) and
+// ix = col_phase (mod col_step) of every pass in p, as values[s][r][c].
+int ipt_oracle_render_rows_values(const ipt_scene* scene, const ipt_params* p, int row_step, int row_phase,
+                                  int col_step, int col_phase, int n_threads, float* values) {
+    if (!scene || !p || !values || row_step <= 0 || row_phase < 0 || col_step <= 0 || col_phase < 0)
+        return IPT_E_INVALID;
+    SceneO sc = make_scene(scene);
+    Mixture mix = build_mixture(sc);
+    Ctx cx{&sc, &mix, p->depth_max};
+    const int W = p->width, H = p->height;
+    std::vector<int> rows;
+    for (int iy = row_phase; iy < H; iy += row_step) rows.push_back(iy);
+    const int64_t nr = (int64_t)rows.size(), nrows = (int64_t)p->spp * nr;
+    const int64_t nc = col_phase < W ? (W - 1 - col_phase) / col_step + 1 : 0;
+    std::atomic<int64_t> next{0};
+    if (n_threads <= 0) n_threads = (int)std::thread::hardware_concurrency();
+    auto work = [&]() {
+        for (;;) {
+            const int64_t r = next.fetch_add(1);
+            if (r >= nrows) break;
+            const int s = (int)(r / nr), q = (int)(r % nr);
+            for (int ix = col_phase, c = 0; ix < W; ix += col_step, ++c) {
+                int xi, yi;
+                values[((int64_t)s * nr + q) * nc + c] = oracle_pixel(cx, p, ix, rows[q], s, &xi, &yi);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return IPT_OK;
+}
 }
 
 extern "C" {

@@ -78,6 +78,26 @@ def render_values(scene_desc: dict, p, n_threads: int = 0, with_counters: bool =
     return out + (cnt.as_dict(),) if with_counters else out
 
 
+def render_rows_values(scene_desc: dict, p, row_step: int, row_phase: int, col_step: int = 1,
+                       col_phase: int = 0, n_threads: int = 0):
+    """Oracle values of the source pixels iy = row_phase (mod row_step),
+    ix = col_phase (mod col_step) of every pass: array [spp][rows][cols] and
+    the row and column indices."""
+    from ipt_amd.capi import make_scene
+
+    lib = load()
+    lib.ipt_oracle_render_rows_values.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                  C.c_int, C.c_void_p]
+    s, keep = make_scene(scene_desc)
+    rows = list(range(row_phase, p.height, row_step))
+    cols = list(range(col_phase, p.width, col_step))
+    vals = np.zeros(p.spp * len(rows) * len(cols), np.float32)
+    rc = lib.ipt_oracle_render_rows_values(C.addressof(s), C.addressof(p), row_step, row_phase, col_step,
+                                           col_phase, n_threads, vals.ctypes.data)
+    assert rc == 0, rc
+    return vals.reshape(p.spp, len(rows), len(cols)), rows, cols
+
+
 def accumulate(values: np.ndarray, codes: np.ndarray, img: dict | None = None):
     """GridRenderPlane::addRay replay; returns dict(pixels, counters, sums, pixel_max)."""
     lib = load()

@@ -440,3 +440,26 @@ def test_axis_aligned_single_light_bit_exact(gpu_ctx, oracle, light):
     gv, gc, ov, oc = _render_both(gpu_ctx, desc, p, oracle)
     assert np.array_equal(gc, oc)
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5", "c3"])
+def test_full_size_rows_bit_exact(gpu_ctx, oracle, cfg):
+    """BASELINE.json configs at their full frame sizes, one pass each (C2: the
+    box at 1024^2, n_rays 16, depth 8; C5: 256 emitters at 2048^2, the light
+    lattice; C3: 10 000 spheres at 1024^2, the sphere grid): every sample of
+    the frame rendered on the GPU, and strided source rows of it recomputed by
+    the oracle, bit-exact; drift codes stay in range."""
+    # (rows, columns) sampled so that the oracle's share stays a few seconds
+    if cfg == "c2":
+        desc, W, rs, rp, cs, cp = scenes.make_scene_box(), 1024, 128, 37, 1, 0
+    elif cfg == "c5":
+        desc, W, rs, rp, cs, cp = scenes.make_scene_box_lights(16), 2048, 1024, 101, 4, 3
+    else:
+        desc, W, rs, rp, cs, cp = scenes.make_scene_spheres(10000, seed=1), 1024, 1024, 517, 32, 5
+    p = capi.make_params(W, W, 1, spp_offset=17, n_rays=16, depth_max=8)
+    gpu_ctx.upload_scene(desc)
+    gv, gc = gpu_ctx.render_values(p)
+    ov, rows, cols = ob.render_rows_values(desc, p, rs, rp, cs, cp, n_threads=16)
+    sel = gv[:, rows, :][:, :, cols]
+    assert np.array_equal(_bits(sel), _bits(ov)), int((_bits(sel) != _bits(ov)).sum())
+    assert (gc != 0xFF).mean() > 0.99
