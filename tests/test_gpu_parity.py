@@ -442,16 +442,18 @@ def test_axis_aligned_single_light_bit_exact(gpu_ctx, oracle, light):
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c5", "c3"])
+@pytest.mark.parametrize("cfg", ["c2", "c4", "c5", "c3"])
 def test_full_size_rows_bit_exact(gpu_ctx, oracle, cfg):
     """BASELINE.json configs at their full frame sizes, one pass each (C2: the
-    box at 1024^2, n_rays 16, depth 8; C5: 256 emitters at 2048^2, the light
-    lattice; C3: 10 000 spheres at 1024^2, the sphere grid): every sample of
-    the frame rendered on the GPU, and strided source rows of it recomputed by
-    the oracle, bit-exact; drift codes stay in range."""
+    box at 1024^2, n_rays 16, depth 8; C4: the box at 4096^2 (one GPU's whole
+    frame); C5: 256 emitters at 2048^2, the light lattice; C3: 10 000 spheres
+    at 1024^2, the sphere grid): every sample of the frame rendered on the GPU,
+    and strided source pixels of it recomputed by the oracle, bit-exact."""
     # (rows, columns) sampled so that the oracle's share stays a few seconds
     if cfg == "c2":
         desc, W, rs, rp, cs, cp = scenes.make_scene_box(), 1024, 128, 37, 1, 0
+    elif cfg == "c4":
+        desc, W, rs, rp, cs, cp = scenes.make_scene_box(), 4096, 1024, 333, 2, 1
     elif cfg == "c5":
         desc, W, rs, rp, cs, cp = scenes.make_scene_box_lights(16), 2048, 1024, 101, 4, 3
     else:
