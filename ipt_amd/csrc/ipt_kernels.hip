@@ -620,9 +620,19 @@ constexpr int kLdsCand = 512;
 // Frames live in LDS, [12][kFrameStride]: column tid is the lane's current
 // sphere-node frame, columns kBlock..kBlock+4 the five wall frames.
 // CosineDdf samples come from exact tables (cos_table_kernel).
-constexpr int kFrameStride = kBlock + 8;
+// Column stride: single-light instances use kBlock + 64 words (a multiple of
+// 64 dwords, so a column's 12 words pair into ds_read2st64/ds_write2st64;
+// 2.7 KiB more, still 4 workgroups/CU); the others keep kBlock + 8 so that
+// their light data fits 4 workgroups as well.
+#ifndef IPT_FS_WIDE
+#define IPT_FS_WIDE 1
+#endif
+__host__ __device__ constexpr int frame_stride(int lmode) {
+    return (IPT_FS_WIDE && (lmode == 1 || lmode == 5 || lmode == 6)) ? kBlock + 64 : kBlock + 8;
+}
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
-    return 12 * (size_t)kFrameStride + (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0);
+    return 12 * (size_t)frame_stride(lmode) +
+           (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0);
 }
 // kLightsGlobal: mixture weights + CDF (and, when small, the light BVH) are
 // staged in LDS after the fixed layout: their global copies would be evicted
@@ -788,6 +798,7 @@ template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
+    constexpr int kFrameStride = frame_stride(LMODE);
     float* lfr = lds + MAXSUSP * kStackFields * kBlock;       // [12][kFrameStride] lane + wall frames
     LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride);
     float* weights_lds = reinterpret_cast<float*>(lights_lds) + kLdsLights * kLightWords;
