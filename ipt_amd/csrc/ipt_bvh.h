@@ -231,7 +231,7 @@ struct SphereGrid {
 };
 
 #ifndef IPT_GRID_CELLS_PER_SPHERE
-#define IPT_GRID_CELLS_PER_SPHERE 3.0
+#define IPT_GRID_CELLS_PER_SPHERE 1.5  // C3 sweep: 0.75-12, best 1.5 with a 5-cell budget
 #endif
 inline bool grid_build_spheres(const float* cr, int n, const float cam[3], float B, SphereGrid& g) {
     if (n <= 0) return false;

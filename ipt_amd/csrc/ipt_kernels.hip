@@ -70,7 +70,7 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #define IPT_RESUME 1  // sphere-BVH walks bounded per step and resumed in later steps
 #endif
 #ifndef IPT_GRID_BUDGET
-#define IPT_GRID_BUDGET 8  // grid cells per lane per step of a resumable walk (measured: 4-32)
+#define IPT_GRID_BUDGET 5  // grid cells per lane per step of a resumable walk (measured: 4-32; 5 with 1.5 cells per sphere)
 #endif
 #ifndef IPT_SPHERE_GRID
 #define IPT_SPHERE_GRID 1  // uniform grid instead of the BVH for large sphere lists inside the box
