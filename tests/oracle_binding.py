@@ -61,6 +61,13 @@ def fptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_float))
 
 
+def _threads(n: int) -> int:
+    """0 = the host's cores, capped at 16 (a GPU box's CPU share)."""
+    import os
+
+    return n if n > 0 else max(1, min(16, os.cpu_count() or 1))
+
+
 def render_values(scene_desc: dict, p, n_threads: int = 0, with_counters: bool = False):
     from ipt_amd.capi import Counters, make_scene
 
@@ -71,7 +78,7 @@ def render_values(scene_desc: dict, p, n_threads: int = 0, with_counters: bool =
     codes = np.zeros(n, np.uint8)
     cnt = Counters()
     rc = lib.ipt_oracle_render_values(C.byref(s), C.byref(p), vals.ctypes.data, codes.ctypes.data,
-                                      n_threads, C.byref(cnt) if with_counters else None)
+                                      _threads(n_threads), C.byref(cnt) if with_counters else None)
     assert rc == 0, rc
     shape = (p.spp, p.height, p.width)
     out = (vals.reshape(shape), codes.reshape(shape))
@@ -93,7 +100,7 @@ def render_rows_values(scene_desc: dict, p, row_step: int, row_phase: int, col_s
     cols = list(range(col_phase, p.width, col_step))
     vals = np.zeros(p.spp * len(rows) * len(cols), np.float32)
     rc = lib.ipt_oracle_render_rows_values(C.addressof(s), C.addressof(p), row_step, row_phase, col_step,
-                                           col_phase, n_threads, vals.ctypes.data)
+                                           col_phase, _threads(n_threads), vals.ctypes.data)
     assert rc == 0, rc
     return vals.reshape(p.spp, len(rows), len(cols)), rows, cols
 
