@@ -54,9 +54,6 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_BFRESOLVE
 #define IPT_BFRESOLVE 1  // resolve's hit/light/expand decision as selects (+1 %)
 #endif
-#ifndef IPT_POPMASK
-#define IPT_POPMASK 1  // multi-level pops from a per-lane finished-levels mask (+3 % C2)
-#endif
 #ifndef IPT_NL1
 #define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
 #endif
@@ -209,27 +206,16 @@ struct KParams {
 #ifndef IPT_SETUP_WAIT
 #define IPT_SETUP_WAIT 1  // drain the setup loads before the step loop
 #endif
-#ifndef IPT_PF
-#define IPT_PF 0  // the iteration prologue one step ahead (measured -1 to -2 %: instruction cost)
-#endif
 #ifndef IPT_FRAME_PF
-#define IPT_FRAME_PF 3  // the next step's frame-table entry gathered a step ahead: 1 at the
-                        // step's end, 2 right after the geometry trace (before resolve)
+#define IPT_FRAME_PF 3  // 3: the next step's frame-table entry gathered at the end of the step
+                        // (0: in the frame pass; gathering it right after the geometry trace,
+                        // or at the step's end with a predicted node, measured slower)
 #endif
 #ifndef IPT_COSB_INLINE
 #define IPT_COSB_INLINE 1  // (cos phi, sin phi) of CosineDdf computed instead of gathered (+11 % C2)
 #endif
 #ifndef IPT_COSB_INLINE_RES
 #define IPT_COSB_INLINE_RES 1  // the same in the resumable (sphere-list, many-light) instances
-#endif
-#ifndef IPT_COSA_INLINE
-#define IPT_COSA_INLINE 0  // with IPT_COSB_INLINE: CosineDdf's r = sin(acos(sqrt(u1))) computed too
-#endif
-#ifndef IPT_FRAME_NT
-#define IPT_FRAME_NT 0  // frame-table gathers with the non-temporal hint
-#endif
-#ifndef IPT_COSA_NT
-#define IPT_COSA_NT 0  // CosineDdf r-table gathers with the non-temporal hint
 #endif
 #ifndef IPT_LIGHT_INR
 #define IPT_LIGHT_INR 1  // ... with the range-free roots / quotients of light_ranges_box
@@ -327,22 +313,10 @@ __device__ __forceinline__ bool owned_row(const KParams& kp, int yi) {
 struct Win8 {
     uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
 };
-__device__ __forceinline__ uint32_t win_at(const Win8& w, uint32_t j) {
-    // j in [0,6)
-    uint32_t lo = j == 0 ? w.a0 : (j == 1 ? w.a1 : (j == 2 ? w.a2 : w.a3));
-    uint32_t hi = j == 4 ? w.b0 : w.b1;
-    return j < 4 ? lo : hi;
-}
 
 // w_j, w_(j+1), w_(j+2) for j in [0,4) (the prologue shifts the window as soon
 // as k leaves block blk, and a step consumes at most 3 draws): three 4-way
 // selects on j's two bits instead of three 6-way chains
-#ifndef IPT_WIN4
-#define IPT_WIN4 1
-#endif
-#ifndef IPT_POP2
-#define IPT_POP2 1  // the pop's LDS reads issued together (see pop_node)
-#endif
 __device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
     const bool b0 = (j & 1u) != 0u, b1 = (j & 2u) != 0u;
     const uint32_t lo = b0 ? x1 : x0, hi = b0 ? x3 : x2;
@@ -917,23 +891,21 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     // never stored: walls load theirs from the LDS table, sphere nodes rebuild
     // theirs (make_frame) in the frame phase of the step after a push or pop.
     bool active = true, has_path = false, fresh = false, need_frame = false, need_b = false;
-    // the next iteration's pick and draws (IPT_PF: prepared one step ahead)
+    // the iteration's pick and draws (prologue) and CosineDdf factors (gathers)
     int pick = -1;
     float u1 = 0.0f, u2 = 0.0f, tr = 0.0f, cs_c = 0.0f, cs_s = 0.0f;
-    bool pf = false;  // pick/u1/u2/cs_* hold the lane's next iteration
-    // IPT_FRAME_PF: the frame-table entry (sin, cos) of the node the lane will
-    // build a frame for in the next step, gathered at the end of this step;
-    // pfz = the to.z bits it belongs to (checked at use)
+    // IPT_FRAME_PF == 3: the frame-table entry (sin, cos) of the node the lane
+    // builds a frame for in the next step, gathered at the end of this step,
+    // with its `to` (pfok: `to` inside the table's range)
     float pfs = 0.0f, pfc = 0.0f;
-    uint32_t pfz = 0xffffffffu;
-    vec3 pto = v3(0, 0, 0);  // IPT_FRAME_PF == 3: the prepared frame's `to`
+    vec3 pto = v3(0, 0, 0);
     bool pfok = false;
     uint32_t unit = 0;  // < 2^32 per launch (checked by the host)
     uint32_t rpass = 0, rpix = 0, k = 0, blk = 0;
     Win8 w;
     vec3 tpos = v3(0, 0, 0);
     int fdepth = -1;  // depth of the sphere node whose frame is in the lane's column
-    uint32_t finm = 0;  // IPT_POPMASK: bit l = the node suspended at level l has run all its iterations
+    uint32_t finm = 0;  // bit l = the node suspended at level l has run all its iterations
     // Resumable sphere-BVH walks (sphere-list scenes): a lane whose walk is not
     // done within IPT_WALK_BUDGET node visits keeps its ray and light results
     // and resumes the walk in the next steps (doing nothing else meanwhile), so
@@ -1008,8 +980,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // same operations on the same state, nothing changes it in between but
         // the refill of lanes without a path)
         auto pop_node = [&]() {
-        if (IPT_POPMASK && active && has_path && !fresh && !((kRes || kResL) && tracing) &&
-            ti >= (kp.n_rays >> tdepth)) {
+        if (active && has_path && !fresh && !((kRes || kResL) && tracing) && ti >= (kp.n_rays >> tdepth)) {
             // the node is done: unwind every suspended level whose node has run
             // all its iterations too (finm, set at push) in one pass -- only
             // their res/multiplier are read -- then resume the first level
@@ -1023,95 +994,45 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             };
             const uint32_t m = ~finm & ((1u << tdepth) - 1u);
             const int stop = m ? 31 - (int)__clz(m) : -1;
-            if (IPT_POP2) {
-                // every LDS read of the unwind issued before the first use -- the
-                // resumed level's six fields and the res/multiplier of the first
-                // two finished levels (addresses clamped to level 0 where a level
-                // does not exist; those values are not used) -- so that their
-                // latencies overlap instead of forming a chain; the outcomes as
-                // selects so that the loads have unconditional consumers
-                auto lvl = [&](int l) { return stk + (size_t)(l < 0 ? 0 : l) * kStackFields * kBlock + tid; };
-                const float* bs = lvl(stop);
-                const float s0 = bs[0 * kBlock], s1 = bs[1 * kBlock], s2 = bs[2 * kBlock];
-                const float s3 = bs[3 * kBlock], s4 = bs[4 * kBlock], s5 = bs[5 * kBlock];
-                const float* b1 = lvl(tdepth - 1);
-                const float r1 = b1[3 * kBlock], m1 = b1[4 * kBlock];
-                const float* b2 = lvl(tdepth - 2);
-                const float r2 = b2[3 * kBlock], m2 = b2[4 * kBlock];
-                auto fin_s = [&](float r, int d) {
-                    const float q = n_pow2 ? r * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - d))
-                                           : r / (float)(kp.n_rays >> (d < 0 ? 0 : d));
-                    return isfinite_(r) ? q : 0.0f;
-                };
-                float v = fin_s(tres, tdepth);
-                const float v1 = fin_s(r1 + (m1 * 1.0f) * v, tdepth - 1);
-                v = tdepth - 1 > stop ? v1 : v;
-                const float v2 = fin_s(r2 + (m2 * 1.0f) * v, tdepth - 2);
-                v = tdepth - 2 > stop ? v2 : v;
-                for (int l = tdepth - 3; l > stop; --l) {
-                    const float* b = lvl(l);
-                    v = fin_v(b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v, l);
-                }
-                const bool resume = stop >= 0;
-                const int meta = __float_as_int(s5);
-                tpos = resume ? v3(s0, s1, s2) : tpos;
-                tres = resume ? s3 + (s4 * 1.0f) * v : tres;  // res += multiplier*albedo*ray_power
-                ti = resume ? meta & 0xff : ti;
-                tkind = resume ? meta >> 8 : tkind;
-                need_frame = resume ? (meta >> 8) >= 5 && fdepth != stop : need_frame;
-                tdepth = resume ? stop : tdepth;
-                if (!resume) {
-                    kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
-                    has_path = false;
-                }
-                return;
-            }
-            float v = fin_v(tres, tdepth);
-            for (int l = tdepth - 1; l > stop; --l) {
-                const float* b = stk + (size_t)l * kStackFields * kBlock + tid;
+            // every LDS read of the unwind issued before the first use -- the
+            // resumed level's six fields and the res/multiplier of the first
+            // two finished levels (addresses clamped to level 0 where a level
+            // does not exist; those values are not used) -- so that their
+            // latencies overlap instead of forming a chain; the outcomes as
+            // selects so that the loads have unconditional consumers
+            auto lvl = [&](int l) { return stk + (size_t)(l < 0 ? 0 : l) * kStackFields * kBlock + tid; };
+            const float* bs = lvl(stop);
+            const float s0 = bs[0 * kBlock], s1 = bs[1 * kBlock], s2 = bs[2 * kBlock];
+            const float s3 = bs[3 * kBlock], s4 = bs[4 * kBlock], s5 = bs[5 * kBlock];
+            const float* b1 = lvl(tdepth - 1);
+            const float r1 = b1[3 * kBlock], m1 = b1[4 * kBlock];
+            const float* b2 = lvl(tdepth - 2);
+            const float r2 = b2[3 * kBlock], m2 = b2[4 * kBlock];
+            auto fin_s = [&](float r, int d) {
+                const float q = n_pow2 ? r * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - d))
+                                       : r / (float)(kp.n_rays >> (d < 0 ? 0 : d));
+                return isfinite_(r) ? q : 0.0f;
+            };
+            float v = fin_s(tres, tdepth);
+            const float v1 = fin_s(r1 + (m1 * 1.0f) * v, tdepth - 1);
+            v = tdepth - 1 > stop ? v1 : v;
+            const float v2 = fin_s(r2 + (m2 * 1.0f) * v, tdepth - 2);
+            v = tdepth - 2 > stop ? v2 : v;
+            for (int l = tdepth - 3; l > stop; --l) {
+                const float* b = lvl(l);
                 v = fin_v(b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v, l);
             }
-            if (stop < 0) {
+            const bool resume = stop >= 0;
+            const int meta = __float_as_int(s5);
+            tpos = resume ? v3(s0, s1, s2) : tpos;
+            tres = resume ? s3 + (s4 * 1.0f) * v : tres;  // res += multiplier*albedo*ray_power
+            ti = resume ? meta & 0xff : ti;
+            tkind = resume ? meta >> 8 : tkind;
+            need_frame = resume ? (meta >> 8) >= 5 && fdepth != stop : need_frame;
+            tdepth = resume ? stop : tdepth;
+            if (!resume) {
                 kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
                 has_path = false;
-            } else {
-                const float* b = stk + (size_t)stop * kStackFields * kBlock + tid;
-                tpos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
-                const int meta = __float_as_int(b[5 * kBlock]);
-                tres = b[3 * kBlock] + (b[4 * kBlock] * 1.0f) * v;  // res += multiplier*albedo*ray_power
-                ti = meta & 0xff;
-                tkind = meta >> 8;
-                tdepth = stop;
-                need_frame = tkind >= 5 && fdepth != stop;
-            }
-        }
-        if (!IPT_POPMASK && active && has_path && !fresh && !((kRes || kResL) && tracing)) {
-            for (;;) {
-                const int n = kp.n_rays >> tdepth;
-                if (ti < n) break;
-                IPT_PHASE(1);
-                float v = 0.0f;
-                if (isfinite_(tres))
-                    v = n_pow2 ? tres * __builtin_amdgcn_ldexpf(1.0f, -(n_log2 - tdepth))
-                               : tres / (float)n;
-                if (tdepth == 0) {
-                    kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
-                    has_path = false;
-                    break;
-                }
-                const int lvl = tdepth - 1;
-                const float* b = stk + (size_t)lvl * kStackFields * kBlock + tid;
-                tpos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
-                const float pres = b[3 * kBlock];
-                const float pmult = b[4 * kBlock];
-                const int meta = __float_as_int(b[5 * kBlock]);
-                tres = pres + (pmult * 1.0f) * v;  // res += multiplier*albedo*ray_power
-                ti = meta & 0xff;
-                tkind = meta >> 8;
-                tdepth = lvl;
-                // a sphere node's frame is still in the lane's column unless a
-                // sphere descendant has overwritten it
-                need_frame = tkind >= 5 && fdepth != lvl;
             }
         }
         };
@@ -1136,11 +1057,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         const bool fneed = need_frame && has_path && !fresh && !((kRes || kResL) && tracing);
         IPT_STAMP_AT(3);  // (new path: later in the step)
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153) and,
-        // for a cosine pick, the CosineDdf table gathers. IPT_PF: run for the
-        // NEXT iteration right after this step's direction phase (the draws are
-        // sequential per path whichever node iterates next), so the gathers have
-        // the rest of the step to land instead of being drained by the frame
-        // pass's wait; the lane carries pick/u1/u2/cs_* to its next iteration.
+        // for a cosine pick, the CosineDdf table gathers (running it one step
+        // ahead, right after the direction phase, measured -2.7 %: DESIGN.md 4.3)
         const bool iter_lane = active && has_path && !fresh && !((kRes || kResL) && tracing);
         // the cosine pick's table indices; the gathers are issued by the whole
         // wave after the prologue (index 0 for the other lanes) so that the
@@ -1174,13 +1092,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
             } else if (IPT_COSB_INLINE) {
                 // (cos phi, sin phi) computed (the table kernel's own code): one
-                // table line per cosine sample instead of two
-                if (IPT_COSA_INLINE)  // r too: no table line at all
-                    tr = sinf_small_(acosf_(sqrt_inrange_(u01(gi_a << 8))));
-                else if (IPT_COSA_NT)
-                    tr = __builtin_nontemporal_load(&kp.cos_a[gcos ? gi_a : 0u]);
-                else
-                    tr = kp.cos_a[gcos ? gi_a : 0u];
+                // table line per cosine sample instead of two (computing r as
+                // well, or non-temporal gathers, measured slower: DESIGN.md 4.3)
+                tr = kp.cos_a[gcos ? gi_a : 0u];
                 float sp, cp;
                 sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
                 cs_c = cp;
@@ -1214,8 +1128,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
                 need_b = false;
             }
-            const uint32_t j = IPT_WIN4 ? (k & 3u) : k - 4 * blk;
-            const float r = u01(IPT_WIN4 ? sel4(j, w.a0, w.a1, w.a2, w.a3) : win_at(w, j));
+            const uint32_t j = k & 3u;  // = k - 4*blk: the window was shifted above
+            const float r = u01(sel4(j, w.a0, w.a1, w.a2, w.a3));
             int c = 0;
             if (one_light(LMODE)) {
                 c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
@@ -1239,8 +1153,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             }
             pick = c;
             if (c <= nl) {
-                const uint32_t r1 = IPT_WIN4 ? sel4(j, w.a1, w.a2, w.a3, w.b0) : win_at(w, j + 1);
-                const uint32_t r2 = IPT_WIN4 ? sel4(j, w.a2, w.a3, w.b0, w.b1) : win_at(w, j + 2);
+                const uint32_t r1 = sel4(j, w.a1, w.a2, w.a3, w.b0);
+                const uint32_t r2 = sel4(j, w.a2, w.a3, w.b0, w.b1);
                 u1 = u01(r1);
                 u2 = u01(r2);
                 if (c == nl) {
@@ -1257,13 +1171,11 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
             }
         };
-        if (!IPT_PF) {
-            if (iter_lane) {
-                IPT_PHASE(3);
-                prologue();
-            }
-            gathers(iter_lane);
+        if (iter_lane) {
+            IPT_PHASE(3);
+            prologue();
         }
+        gathers(iter_lane);
         // (the frame build sits between the table gathers' issue and their use)
         // ------------- phase 3: the current node's RotateDdf frame when it is a sphere node without one
         // (after a push, or a pop past a sphere descendant): built by the lane
@@ -1307,18 +1219,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                                 keep_alive(fc);
                             }
                         pfok = false;
-                    } else if (kFramePf) {
-                        to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
-                        // normally gathered at the end of the previous step
-                        const bool have = f2u(to.z) == pfz;
-                        fs = pfs;
-                        fc = pfc;
-                        if (__builtin_expect(__any(!have), 0))
-                            if (!have) {
-                                frame_sc_lookup(kp.frame_sc, to, fs, fc);
-                                keep_alive(fs);  // its wait stays in this rare branch
-                                keep_alive(fc);
-                            }
                     } else {
                         to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
                         frame_sc_lookup(kp.frame_sc, to, fs, fc);
@@ -1398,7 +1298,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     blk = 0;
                     need_b = true;  // block 1 is produced by the window refill of the next iteration
                     k = 2;
-                    pf = false;
                     rdepth = 0;
                     have_ray = true;
                     if (COUNT) ++c_paths;
@@ -1414,7 +1313,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             blk = 0;
             need_b = true;
             k = 2;
-            pf = false;
             if (COUNT && g.drift) ++c_drift;
             if (!g.valid) {
                 has_path = false;
@@ -1480,17 +1378,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 have_ray = true;
                 is_iter = true;
             }
-            pf = false;
-        }
-        if (IPT_PF) {
-            const bool ran = active && has_path && !pf;
-            if (ran) {
-                // the next iteration of this path (incl. a new path's first)
-                IPT_PHASE(3);
-                prologue();
-                pf = true;
-            }
-            gathers(ran);
         }
         IPT_STAMP_AT(8);  // direction
         // --------------------------------------------- phase 4: trace + resolve
@@ -1554,8 +1441,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             if (push) {
                 IPT_PHASE(10);
                 if (iter) {
-                    if (IPT_POPMASK)
-                        finm = (finm & ~(1u << tdepth)) | ((ti >= (kp.n_rays >> tdepth) ? 1u : 0u) << tdepth);
+                    finm = (finm & ~(1u << tdepth)) | ((ti >= (kp.n_rays >> tdepth) ? 1u : 0u) << tdepth);
                     float* b = stk + (size_t)tdepth * kStackFields * kBlock + tid;
                     b[0 * kBlock] = tpos.x;
                     b[1 * kBlock] = tpos.y;
@@ -1676,13 +1562,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
             }
         } else {
-        // IPT_FRAME_PF == 2: the trace's results wait for resolve until the next
-        // node's frame-table gather has been issued (see below)
-        constexpr bool kFramePf2 = kFramePf == 2 && IPT_FRAME_TAB && kFrameInrange;
-        bool rs_do = false, rs_has_li = false;
-        float rs_t = inf_(), rs_mult = 0.0f, rs_li_pow = 0.0f;
-        int rs_prim = -1;
-        vec3 rs_li_pos = v3(0, 0, 0);
         if (have_ray) {
             IPT_PHASE(8);
             // lights: per-light traces feed both UnionDdf::value (ddf.cpp:157-162)
@@ -1836,73 +1715,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     }
                     IPT_STAMP_AT(10);  // mixture value + geometry trace
                 }
-                if (kFramePf2) {
-                    rs_do = true;
-                    rs_t = t;
-                    rs_prim = prim;
-                    rs_mult = mult;
-                    rs_has_li = has_li;
-                    rs_li_pos = li_pos;
-                    rs_li_pow = li_pow;
-                } else {
-                    resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
-                }
+                resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
             }
         }
         IPT_STAMP_AT(11);  // resolve + push
-        if constexpr (kFramePf2) {
-            // the node current at the next step and whether its frame is built
-            // then -- a sphere node this ray pushes (resolve's decision, computed
-            // the same way), or the pop target (the first unfinished ancestor, as
-            // the pop computes it) when the node has run all its iterations and a
-            // descendant overwrote that node's column -- and its frame-table
-            // gather, issued now so that resolve, the pop and the next step's
-            // prologue cover its latency (the frame build's only memory access)
-            bool want = false, push = false;
-            vec3 ppos = v3(0, 0, 0);
-            if (active && has_path) {
-                if (rs_do) {
-                    const bool has_si = rs_prim >= 0;
-                    const vec3 si_pos = ro + rd * rs_t;
-                    const vec3 ea = si_pos - ro, eb = rs_li_pos - ro;
-                    const bool lg = (rs_has_li && has_si) ? longer_sq(dot(ea, ea), dot(eb, eb)) : false;
-                    const bool li_wins = rs_has_li && (!has_si || lg);
-                    push = rdepth < kp.depth_max && !li_wins && has_si && (kp.n_rays >> rdepth) != 0;
-                    if (push && rs_prim >= 5) {
-                        want = true;
-                        ppos = si_pos;
-                    }
-                }
-                if (!push && (is_iter || !rs_do) && ti >= (kp.n_rays >> tdepth)) {
-                    const uint32_t m = ~finm & ((1u << tdepth) - 1u);
-                    const int stop = m ? 31 - (int)__clz(m) : -1;
-                    if (stop >= 0 && fdepth != stop) {
-                        const float* b = stk + (size_t)stop * kStackFields * kBlock + tid;
-                        if ((__float_as_int(b[5 * kBlock]) >> 8) >= 5) {
-                            want = true;
-                            ppos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
-                        }
-                    }
-                }
-            }
-            uint32_t idx = 0, u = 0xffffffffu;
-            if (want) {
-                const vec3 to = normalize_inrange_(ppos);
-                u = f2u(to.z);
-                const uint32_t mz = u & 0x7fffffffu;
-                if (mz - kFrameTabLo <= kFrameTabSpan) idx = ((mz - kFrameTabLo) << 1) | (u >> 31);
-                else u = 0xffffffffu;
-            }
-            // issued by the whole wave (index 0 for the other lanes, whose pfz
-            // marks the entry unused) and consumed in the next step's frame pass
-            const float2 e = kp.frame_sc[idx];
-            pfs = e.x;
-            pfc = e.y;
-            pfz = u;
-            if (rs_do)
-                resolve(rdepth < kp.depth_max, rs_t, rs_prim, ro, rd, rdepth, is_iter, rs_mult, rs_has_li, rs_li_pos,
-                        rs_li_pow);
-        }
         if (kRes && tracing) {
             IPT_PHASE(9);
             bool done;
@@ -1932,14 +1748,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     const uint32_t u = f2u(to.z), mz = u & 0x7fffffffu;
                     pfok = mz - kFrameTabLo <= kFrameTabSpan;
                     if (pfok) {
-#if IPT_FRAME_NT
-                        typedef float f2v __attribute__((ext_vector_type(2)));
-                        const f2v ev = __builtin_nontemporal_load(
-                            reinterpret_cast<const f2v*>(&kp.frame_sc[((mz - kFrameTabLo) << 1) | (u >> 31)]));
-                        const float2 e = make_float2(ev.x, ev.y);
-#else
                         const float2 e = kp.frame_sc[((mz - kFrameTabLo) << 1) | (u >> 31)];
-#endif
                         pfs = e.x;
                         pfc = e.y;
                         pto = to;
@@ -1947,46 +1756,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 }
             }
             IPT_STAMP_AT(7);  // next frame's `to` + table gather
-        }
-        if constexpr (kFramePf == 1 && IPT_FRAME_TAB && kFrameInrange) {
-            // the node current at the next step and whether its frame is built
-            // then: a sphere node pushed this step, or the pop target (the first
-            // unfinished ancestor, as the pop computes it) when this node has run
-            // all its iterations and a descendant overwrote that node's column.
-            // Its frame-table entry is gathered now, a step before the frame
-            // pass needs it (the gather is the frame build's only memory access).
-            bool want = false;
-            vec3 ppos = tpos;
-            if (active && has_path && !fresh) {
-                if (need_frame) {
-                    want = true;
-                } else if (ti >= (kp.n_rays >> tdepth)) {
-                    const uint32_t m = ~finm & ((1u << tdepth) - 1u);
-                    const int stop = m ? 31 - (int)__clz(m) : -1;
-                    if (stop >= 0 && fdepth != stop) {
-                        const float* b = stk + (size_t)stop * kStackFields * kBlock + tid;
-                        const int kind = __float_as_int(b[5 * kBlock]) >> 8;
-                        if (kind >= 5) {
-                            want = true;
-                            ppos = v3(b[0 * kBlock], b[1 * kBlock], b[2 * kBlock]);
-                        }
-                    }
-                }
-            }
-            uint32_t idx = 0, u = 0xffffffffu;
-            if (want) {
-                const vec3 to = normalize_inrange_(ppos);
-                u = f2u(to.z);
-                const uint32_t mz = u & 0x7fffffffu;
-                if (mz - kFrameTabLo <= kFrameTabSpan) idx = ((mz - kFrameTabLo) << 1) | (u >> 31);
-                else u = 0xffffffffu;
-            }
-            // issued by the whole wave (index 0 for the other lanes, whose pfz
-            // marks the entry unused) and consumed in the next step's frame pass
-            const float2 e = kp.frame_sc[idx];
-            pfs = e.x;
-            pfc = e.y;
-            pfz = u;
         }
     }
 

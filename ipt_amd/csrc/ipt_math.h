@@ -377,23 +377,9 @@ IPT_HD float cosf_(float y) {
 // polynomial is odd in x, and round-to-nearest is symmetric, so the results
 // are exactly sg * cos_poly(c_i) and s * sin_poly(x): two sign flips of the
 // float results instead of selected f64 constants (same bits for every input).
-#ifndef IPT_SINCOS_SIGNLAST
-#define IPT_SINCOS_SIGNLAST 1
-#endif
 IPT_HD void sincosf_small_(float y, float* sp, float* cp) {
     int n;
     const double x = reduce_fast_((double)y, &n);
-    if (!IPT_SINCOS_SIGNLAST) {  // glibc's form (A/B builds)
-        const double s = sincos_sign(n & 3);
-        const sincos_tab p = sincos_table((n & 2) ? 1 : 0);
-        const double x2 = x * x;
-        const float a = sin_poly_(x * s, x2, p);
-        const float b = cos_poly_(x2, p);
-        const bool tiny = abstop12(y) < abstop12(0x1p-12f);
-        *sp = tiny ? y : ((n & 1) ? b : a);
-        *cp = tiny ? 1.0f : ((n & 1) ? a : b);
-        return;
-    }
     const sincos_tab p = sincos_table(0);
     const double x2 = x * x;
     const uint32_t s_neg = ((n & 3) == 1 || (n & 3) == 2) ? 0x80000000u : 0u;  // sincos_sign(n & 3)

@@ -220,16 +220,13 @@ IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
 // (0, 2^-96), outside the root's range, only when B = 0 and A < 2^-98, i.e.
 // |b| < 2^-48: sd < 2^-45 with either root, both roots fall below 1e-6 and the
 // test misses either way. desc is never -0 (A >= +0); desc < 2^84.
-#ifndef IPT_SPHERE_INR
-#define IPT_SPHERE_INR 1
-#endif
 template <bool BF = false, bool INR = false>
 IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
     const float b = dot(o, d);
-    const float desc = (INR && IPT_SPHERE_INR) ? 4.0f * (b * b - (dot(o, o) - radius * radius))
+    const float desc = INR ? 4.0f * (b * b - (dot(o, o) - radius * radius))
                                                : 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
     if (BF) {
-        const float sd = (INR && IPT_SPHERE_INR) ? sqrt_inrange_(desc) : sqrt_(desc);
+        const float sd = INR ? sqrt_inrange_(desc) : sqrt_(desc);
         const float m2b = -2.0f * b;
         float t1 = (m2b - sd) * 0.5f;
         float t2 = (m2b + sd) * 0.5f;
@@ -258,12 +255,6 @@ IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
 // zero): dp = sgn*d_a equals |d_a| whenever |dp| >= 1e-6 (otherwise the test
 // misses either way), so `dp < 0` never decides, and 1 - sgn*o_a is one
 // rounding of an exact product, i.e. fma(-sgn, o_a, 1). Same t, same miss.
-#ifndef IPT_BOXPLANES
-#define IPT_BOXPLANES 1
-#endif
-#ifndef IPT_BOXSEL
-#define IPT_BOXSEL 1
-#endif
 template <bool INRANGE>
 IPT_HD float facing_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
     const float dp = fabs_(da);
@@ -280,7 +271,7 @@ IPT_HD float facing_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
 // reference's order {+x,+y,+z,-x,-z}, 5 = the r=0.5 sphere.
 template <bool INRANGE = false>
 IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
-    if (IPT_BOXPLANES && IPT_BRANCHFREE) {
+    if (IPT_BRANCHFREE) {
         // a NaN direction fails every test (the reference returns no hit);
         // the planes are computed regardless and the result selected at the end
         const bool dnan = d.x + d.y + d.z != d.x + d.y + d.z;
@@ -291,18 +282,14 @@ IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
         const float ty = d.y > 0.0f ? ty0 : inf_();
         // the scan's "nearer, or as near with a lower index" as selects (bitwise
         // on the comparisons: no short-circuit control flow)
-        if (IPT_BOXSEL) {
-            const bool take_y = (ty < best) | ((ty == best) & (1 < bi) & (ty != inf_()));
-            best = take_y ? ty : best;
-            bi = take_y ? 1 : bi;
-        } else if (ty < best || (ty == best && 1 < bi && ty != inf_())) { best = ty; bi = 1; }
+        const bool take_y = (ty < best) | ((ty == best) & (1 < bi) & (ty != inf_()));
+        best = take_y ? ty : best;
+        bi = take_y ? 1 : bi;
         const float tz = facing_plane_t<INRANGE>(o.z, d.z, zp ? 1.0f : -1.0f, o, d);
         const int iz = zp ? 2 : 4;
-        if (IPT_BOXSEL) {
-            const bool take_z = (tz < best) | ((tz == best) & (iz < bi) & (tz != inf_()));
-            best = take_z ? tz : best;
-            bi = take_z ? iz : bi;
-        } else if (tz < best || (tz == best && iz < bi && tz != inf_())) { best = tz; bi = iz; }
+        const bool take_z = (tz < best) | ((tz == best) & (iz < bi) & (tz != inf_()));
+        best = take_z ? tz : best;
+        bi = take_z ? iz : bi;
         const bool none = dnan | (best == inf_());
         *prim = none ? -1 : bi;
         return dnan ? inf_() : best;
