@@ -1271,8 +1271,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         const float* frc = lfr + (tkind < 5 ? kBlock + tkind : tid);
 
         bool have_ray = false, is_iter = false;
-        vec3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
-        int rdepth = 0;
+        // (written by the new-path or the direction phase wherever have_ray is
+        // set and read only then: left uninitialised, no per-step moves)
+        vec3 ro, rd;
+        int rdepth;
         // ------------- phase 2: new path (render_sample body, main.cpp:192-211), after
         // barrier B so that its camera ray is not live across the worker pass
         if (active && has_path && fresh) {
