@@ -69,6 +69,12 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_GRID_BUDGET
 #define IPT_GRID_BUDGET 5  // grid cells per lane per step of a resumable walk (measured: 4-32; 5 with 1.5 cells per sphere)
 #endif
+#ifndef IPT_LPF
+#define IPT_LPF 1  // lattice instances: the picked light's sample fields gathered in the prologue (C5 +2 %)
+#endif
+#ifndef IPT_LPF_BF
+#define IPT_LPF_BF 0  // lattice instances with IPT_LPF: branch-free direction select as kLightsOne
+#endif
 #ifndef IPT_GRID_PIPE
 #define IPT_GRID_PIPE 1  // resumable grid walk pipelined: next cell's range + IPT_GRID_ITEMS item loads in flight (C3 +11 %)
 #endif
@@ -1151,6 +1157,12 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // path and the compiler's waits drain only what they wait for
         uint32_t gi_a = 0, gi_b = 0;
         bool gcos = false;
+        // IPT_LPF (lattice instances): the picked light's sample fields are
+        // gathered with the CosineDdf gathers (whole wave, index 0 for lanes
+        // without a light pick) instead of read in the direction phase
+        vec3 lpP = v3(0, 0, 0);
+        float lpx = 0.0f, lpy = 0.0f, lpn = 0.0f;
+        int lptype = 0;
         // (`ran`: the lane ran the prologue in this step. In the resumable
         // instances a lane keeps its prepared iteration while its walk goes on,
         // so there the gathers stay per lane.)
@@ -1176,6 +1188,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     }
                 }
             } else if (IPT_COSB_INLINE) {
+                if constexpr (grid_lights(LMODE) && IPT_LPF) {
+                    constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                    const LightDev& Ls = kp.lights[(ran && pick >= 0 && pick < nl) ? pick : 0];
+                    lpP = Ls.P;
+                    lpx = comp<XA>(Ls.x);
+                    lpy = comp<YA>(Ls.y);
+                    lpn = comp<2>(Ls.n);
+                    lptype = Ls.type;
+                }
                 // (cos phi, sin phi) computed (the table kernel's own code): one
                 // table line per cosine sample instead of two (computing r as
                 // well, or non-temporal gathers, measured slower: DESIGN.md 4.3)
@@ -1420,14 +1441,21 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         vec3 dir_bf = v3(0, 0, 0);
         // (the lattice instances measured 3 % slower this way: their light sample
         // reads the picked light's record, and both directions cost more there)
-        constexpr bool kDirBf = one_light(LMODE);
+        constexpr bool kGridLpf = grid_lights(LMODE) && IPT_LPF;
+        constexpr bool kDirBf = one_light(LMODE) || (kGridLpf && IPT_LPF_BF);
         if constexpr (kDirBf) {
             Frame fm;
             fm.m0 = v3(frc[0 * kFrameStride], frc[1 * kFrameStride], frc[2 * kFrameStride]);
             fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
             fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
             const vec3 cdir = frame_apply(fm, v3(tr * cs_c, tr * cs_s, sqrt_inrange_(u1)));
-            const vec3 ldir = lsample(LS.one, tpos, u1, u2);
+            vec3 ldir;
+            if constexpr (kGridLpf) {
+                constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                ldir = light_sample_dir_axf<XA, YA, IPT_LIGHT_INR>(lpP, lpx, lpy, lpn, lptype, tpos, u1, u2);
+            } else {
+                ldir = lsample(LS.one, tpos, u1, u2);
+            }
             if (IPT_ABL == 7) keep_alive(lsample(LS.one, tpos, u1 + kp.abl_zero, u2));
             const vec3 zero = v3(0, 0, 0);
             dir_bf = pick < nl ? ldir : (pick == nl ? cdir : zero);
@@ -1439,6 +1467,11 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (COUNT && pick < nl) ++c_lsamp;
             } else if (pick < nl) {
                 IPT_PHASE(7);
+                if constexpr (grid_lights(LMODE) && IPT_LPF) {
+                    // the gathered fields are all light_sample_dir_ax reads
+                    constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                    dir = light_sample_dir_axf<XA, YA, IPT_LIGHT_INR>(lpP, lpx, lpy, lpn, lptype, tpos, u1, u2);
+                } else
                 dir = lsample(LS.light(pick), tpos, u1, u2);
                 if (IPT_ABL == 7)
                     keep_alive(light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1 + kp.abl_zero, u2));

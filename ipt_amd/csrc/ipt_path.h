@@ -522,6 +522,22 @@ IPT_HD float light_pdf_ax(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nr
 // (x*u1 + y*u2) + P keeps one product per component (P's components are
 // non-zero, so a zero product is an exact no-op), cosinus one term (compared
 // with 1e-5 only)
+// light_sample_dir_ax from the light's fields it reads (P, x[XA], y[YA],
+// n[NA], type), for callers that gathered them ahead (same operations)
+template <int XA, int YA, bool INR = false>
+IPT_HD vec3 light_sample_dir_axf(vec3 P, float xa, float ya, float nn, int type, vec3 o, float u1, float u2raw) {
+    constexpr int NA = 3 - XA - YA;
+    const float u2 = u2raw * (type == 1 ? 1.0f - u1 : 1.0f);
+    float pc[3];
+    pc[XA] = xa * u1 + comp<XA>(P);
+    pc[YA] = ya * u2 + comp<YA>(P);
+    pc[NA] = comp<NA>(P);
+    // INR: |pos - o| in [dmin, dmax] for every surface point o
+    const vec3 dir = INR ? normalize_inrange_(v3(pc[0], pc[1], pc[2]) - o) : normalize(v3(pc[0], pc[1], pc[2]) - o);
+    const float cosinus = nn * -comp<NA>(dir);
+    if (cosinus < 1e-5f) return v3(0.0f, 0.0f, 0.0f);
+    return dir;
+}
 template <int XA, int YA, bool INR = false>
 IPT_HD vec3 light_sample_dir_ax(const LightDev& L, vec3 o, float u1, float u2raw) {
     constexpr int NA = 3 - XA - YA;
