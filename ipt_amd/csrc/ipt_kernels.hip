@@ -72,9 +72,6 @@ constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOC
 #ifndef IPT_LPF
 #define IPT_LPF 1  // lattice instances: the picked light's sample fields gathered in the prologue (C5 +2 %)
 #endif
-#ifndef IPT_LPF_BF
-#define IPT_LPF_BF 0  // lattice instances with IPT_LPF: branch-free direction select as kLightsOne
-#endif
 #ifndef IPT_GRID_PIPE
 #define IPT_GRID_PIPE 1  // resumable grid walk pipelined: next cell's range + IPT_GRID_ITEMS item loads in flight (C3 +11 %)
 #endif
@@ -1441,21 +1438,14 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         vec3 dir_bf = v3(0, 0, 0);
         // (the lattice instances measured 3 % slower this way: their light sample
         // reads the picked light's record, and both directions cost more there)
-        constexpr bool kGridLpf = grid_lights(LMODE) && IPT_LPF;
-        constexpr bool kDirBf = one_light(LMODE) || (kGridLpf && IPT_LPF_BF);
+        constexpr bool kDirBf = one_light(LMODE);
         if constexpr (kDirBf) {
             Frame fm;
             fm.m0 = v3(frc[0 * kFrameStride], frc[1 * kFrameStride], frc[2 * kFrameStride]);
             fm.m1 = v3(frc[3 * kFrameStride], frc[4 * kFrameStride], frc[5 * kFrameStride]);
             fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
             const vec3 cdir = frame_apply(fm, v3(tr * cs_c, tr * cs_s, sqrt_inrange_(u1)));
-            vec3 ldir;
-            if constexpr (kGridLpf) {
-                constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
-                ldir = light_sample_dir_axf<XA, YA, IPT_LIGHT_INR>(lpP, lpx, lpy, lpn, lptype, tpos, u1, u2);
-            } else {
-                ldir = lsample(LS.one, tpos, u1, u2);
-            }
+            const vec3 ldir = lsample(LS.one, tpos, u1, u2);
             if (IPT_ABL == 7) keep_alive(lsample(LS.one, tpos, u1 + kp.abl_zero, u2));
             const vec3 zero = v3(0, 0, 0);
             dir_bf = pick < nl ? ldir : (pick == nl ? cdir : zero);
