@@ -109,6 +109,17 @@ inline M3 rotate_identity(float angle, V3 v) {
 
 const float INF = std::numeric_limits<float>::infinity();
 
+// --------------------------------------------------------------- counters
+struct Counters {
+    uint64_t paths = 0, traced = 0, surf = 0, light = 0, expanded = 0, iters = 0, lsamp = 0,
+             skipped = 0, sframes = 0, ltraces = 0, drifted = 0;
+    // SURVEY.md Appendix C's instrumented-reference counts: node sums that are
+    // not finite when main.cpp:181 tests them (the NaN-poison), multipliers
+    // that are not finite where main.cpp:175 asserts, randf() draws
+    uint64_t nf_sums = 0, nf_mults = 0, draws = 0;
+};
+thread_local Counters* g_cnt = nullptr;
+
 // ------------------------------------------------------------------ RNG
 // The randf() replacement (reference include/randf.h:6-11): a per-path
 // sequential stream. Draw k of path (pixel p, pass s) is word k%4 of
@@ -141,6 +152,7 @@ thread_local const float* g_ufeed = nullptr;
 float randf() {
     if (g_ufeed) return *g_ufeed++;
     Rng& g = *g_rng;
+    if (g_cnt) ++g_cnt->draws;
     uint32_t b = g.k >> 2;
     if (b != g.blk_id) {
         uint32_t c[4] = {b, g.s, g.p, 0u};
@@ -154,12 +166,6 @@ float randf() {
     return res;  // never 1.0f, randf.h:8-9's retry never fires
 }
 
-// --------------------------------------------------------------- counters
-struct Counters {
-    uint64_t paths = 0, traced = 0, surf = 0, light = 0, expanded = 0, iters = 0, lsamp = 0,
-             skipped = 0, sframes = 0, ltraces = 0, drifted = 0;
-};
-thread_local Counters* g_cnt = nullptr;
 
 // ------------------------------------------------------------------ scene
 struct AreaLightO {
@@ -588,10 +594,12 @@ float ray_power(const Ctx& cx, V3 origin, V3 direction, int depth, int n_rays) {
         mix_val += w[nl] * sdf.value(new_direction);
         float sdf_val = sdf.value(new_direction);
         float multiplier = sdf_val / mix_val;
+        if (g_cnt && !std::isfinite(multiplier)) ++g_cnt->nf_mults;  // main.cpp:175's assert
         const float albedo = 1.0f;
         res += multiplier * albedo *
                ray_power(cx, si.position, new_direction, depth + 1, n_rays / 2);
     }
+    if (g_cnt && !std::isfinite(res)) ++g_cnt->nf_sums;  // main.cpp:181
     res = std::isfinite(res) ? res / n_rays : 0.0f;
     return res;
 }
@@ -655,6 +663,16 @@ static float oracle_pixel(const Ctx& cx, const ipt_params* p, int ix, int iy, in
     return value;
 }
 
+// GridRenderPlane target (xi, yi) of source pixel (ix, iy) relative to its
+// nominal destination (ix, max(H-2-iy, 0)), as ipt_render_values' codes.
+static uint8_t drift_code(int W, int H, int ix, int iy, int xi, int yi) {
+    const int yn = H - 2 - iy > 0 ? H - 2 - iy : 0;
+    const int dx = xi - ix, dy = yi - yn;
+    uint8_t code = 0xff;
+    if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < W && yi < H) code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
+    return code;
+}
+
 // values/codes: [spp][H][W]; codes as in ipt_render_values. counters may be NULL.
 int ipt_oracle_render_values(const ipt_scene* scene, const ipt_params* p, float* values,
                              uint8_t* codes, int n_threads, ipt_counters* counters) {
@@ -677,11 +695,7 @@ int ipt_oracle_render_values(const ipt_scene* scene, const ipt_params* p, float*
             for (int ix = 0; ix < W; ++ix) {
                 int xi, yi;
                 float v = oracle_pixel(cx, p, ix, iy, s, &xi, &yi);
-                int yn = H - 2 - iy > 0 ? H - 2 - iy : 0;
-                int dx = xi - ix, dy = yi - yn;
-                uint8_t code = 0xff;
-                if (dx >= -1 && dx <= 1 && dy >= -1 && dy <= 1 && xi < W && yi < H)
-                    code = (uint8_t)((dx + 1) | ((dy + 1) << 2));
+                const uint8_t code = drift_code(W, H, ix, iy, xi, yi);
                 if (g_cnt && code != 0x05) ++g_cnt->drifted;
                 int64_t idx = ((int64_t)s * H + iy) * W + ix;
                 values[idx] = v;
@@ -962,6 +976,61 @@ void ipt_oracle_cosine_samples(uint64_t seed, const float* to, int n, float* out
 float ipt_oracle_cosine_ddf_value(const float* to, const float* d) {
     RotatedCosine r(mk(to[0], to[1], to[2]));
     return r.value(mk(d[0], d[1], d[2]));
+}
+}
+
+extern "C" {
+// Per-path event counts (SURVEY.md Appendix C vocabulary) for the statistical
+// pin of the estimator (tests/test_oracle_stats.py): for every path of
+// render_values' order, values[i] (clamped root value) and
+// ev[i*IPT_ORACLE_NEV + e] for e = traced rays, geometry hits, light hits,
+// expanded nodes, iterations, light-sampled iterations, skipped iterations,
+// AreaLight::traceRay calls, non-finite node sums (main.cpp:181), non-finite
+// multipliers (main.cpp:175), randf() draws.
+#define IPT_ORACLE_NEV 11
+int ipt_oracle_nev(void) { return IPT_ORACLE_NEV; }
+int ipt_oracle_render_events(const ipt_scene* scene, const ipt_params* p, int n_threads, float* values,
+                             uint8_t* codes, uint32_t* ev) {
+    if (!scene || !p || !values || !codes || !ev || p->width <= 0 || p->height <= 0 || p->spp < 0) return IPT_E_INVALID;
+    SceneO sc = make_scene(scene);
+    Mixture mix = build_mixture(sc);
+    Ctx cx{&sc, &mix, p->depth_max};
+    const int W = p->width, H = p->height;
+    const int64_t rows = (int64_t)p->spp * H;
+    std::atomic<int64_t> next{0};
+    if (n_threads <= 0) n_threads = (int)std::thread::hardware_concurrency();
+    auto work = [&]() {
+        for (;;) {
+            int64_t r = next.fetch_add(1);
+            if (r >= rows) break;
+            int s = (int)(r / H), iy = (int)(r % H);
+            for (int ix = 0; ix < W; ++ix) {
+                Counters c;
+                g_cnt = &c;
+                int xi, yi;
+                const float v = oracle_pixel(cx, p, ix, iy, s, &xi, &yi);
+                g_cnt = nullptr;
+                const int64_t idx = ((int64_t)s * H + iy) * W + ix;
+                values[idx] = v;
+                codes[idx] = drift_code(W, H, ix, iy, xi, yi);
+                const uint64_t e[IPT_ORACLE_NEV] = {c.traced, c.surf, c.light, c.expanded, c.iters, c.lsamp,
+                                                    c.skipped, c.ltraces, c.nf_sums, c.nf_mults, c.draws};
+                for (int q = 0; q < IPT_ORACLE_NEV; ++q) ev[idx * IPT_ORACLE_NEV + q] = (uint32_t)e[q];
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return IPT_OK;
+}
+
+// Philox4x32-10 block (the randf() replacement's generator) for known-answer
+// tests against Random123's published vectors: out = philox(ctr[4], key[2]).
+void ipt_oracle_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    philox(c, key[0], key[1]);
+    for (int i = 0; i < 4; ++i) out[i] = c[i];
 }
 }
 

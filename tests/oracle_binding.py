@@ -151,3 +151,40 @@ def area_light_struct(P, x, y, power, typ):
     a.power = float(power)
     a.type = int(typ)
     return a
+
+
+EVENT_NAMES = ("traced_rays", "surface_hits", "light_hits", "expanded_nodes", "iterations", "light_samples",
+               "skipped", "light_traces", "nonfinite_sums", "nonfinite_mults", "draws")
+
+
+def render_events(scene_desc: dict, p, n_threads: int = 0):
+    """Per-path values and drift codes [spp][H][W] and event counts
+    [spp][H][W][len(EVENT_NAMES)] (ipt_oracle_render_events)."""
+    from ipt_amd.capi import make_scene
+
+    lib = load()
+    lib.ipt_oracle_render_events.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
+    assert lib.ipt_oracle_nev() == len(EVENT_NAMES)
+    s, keep = make_scene(scene_desc)
+    n = p.spp * p.width * p.height
+    vals = np.zeros(n, np.float32)
+    codes = np.zeros(n, np.uint8)
+    ev = np.zeros((n, len(EVENT_NAMES)), np.uint32)
+    rc = lib.ipt_oracle_render_events(C.addressof(s), C.addressof(p), _threads(n_threads), vals.ctypes.data,
+                                      codes.ctypes.data, ev.ctypes.data)
+    assert rc == 0, rc
+    shape = (p.spp, p.height, p.width)
+    return vals.reshape(shape), codes.reshape(shape), ev.reshape(shape + (len(EVENT_NAMES),))
+
+
+def philox(ctr, key):
+    """Philox4x32-10 block of the oracle's RNG (ipt_oracle_philox)."""
+    lib = load()
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    out = np.zeros(4, np.uint32)
+    lib.ipt_oracle_philox.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.ipt_oracle_philox.restype = None
+    lib.ipt_oracle_philox(c.ctypes.data, k.ctypes.data, out.ctypes.data)
+    return out
