@@ -275,6 +275,12 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
          zero terms against the exact build, over directions hashed from
          the bit pattern (incl. zero / tiny x and y) */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
+/* Philox4x32-10 blocks exactly as the kernels generate the per-path stream
+   that replaces randf() (include/randf.h:6-11; draw k of path (pass s, pixel
+   p) is word k%4 of philox({k/4, s, p, 0}, {seed lo, seed hi})), for
+   known-answer tests: out[4i..4i+3] = philox(ctr[4i..4i+3], {key0, key1}).
+   ctx NULL: the host build of the same code; otherwise on ctx's device. */
+int ipt_philox(ipt_ctx* ctx, uint32_t key0, uint32_t key1, const uint32_t* ctr, uint32_t* out, int64_t n);
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
 /* Device self-check of the fast math paths: for every float bit pattern b in
  * [lo_bits, hi_bits) (hi_bits <= 2^32) compares function fn as the kernels

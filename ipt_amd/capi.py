@@ -88,6 +88,7 @@ EXPORTED_SYMBOLS = (
     "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
     "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck", "ipt_smooth", "ipt_glare", "ipt_ddf_sample", "ipt_ddf_value",
+    "ipt_philox",
 )
 
 # path-kernel phases of the IPT_PROF profile (ipt_kernels.hip IPT_PHASE ids)
@@ -141,6 +142,7 @@ def load(path: str | os.PathLike | None = None):
     lib.ipt_math_host.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
     lib.ipt_math_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64]
     lib.ipt_shard_plan.argtypes = [C.POINTER(Params), C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)]
+    lib.ipt_philox.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int64]
     if path is None:
         _lib = lib
     return lib
@@ -312,6 +314,19 @@ class Context:
         out = np.empty_like(x)
         _check(self.lib, self.h, self.lib.ipt_math_device(self.h, fn, x.ctypes.data, out.ctypes.data, x.size))
         return out
+
+
+def philox(ctr, key, ctx: "Context | None" = None) -> np.ndarray:
+    """Philox4x32-10 blocks as the kernels compute them (ipt_philox): ctr
+    [n][4] uint32, key (k0, k1); ctx None = the library's host build."""
+    lib = load()
+    c = np.ascontiguousarray(np.asarray(ctr, np.uint32).reshape(-1, 4))
+    out = np.zeros_like(c)
+    h = ctx.h if ctx is not None else None
+    rc = lib.ipt_philox(h, int(key[0]), int(key[1]), c.ctypes.data, out.ctypes.data, len(c))
+    if rc != IPT_OK:
+        raise IptError(rc, lib.ipt_last_error(h).decode(errors="replace") if h else "ipt_philox")
+    return out
 
 
 def math_host(fn: int, x: np.ndarray) -> np.ndarray:

@@ -2060,6 +2060,16 @@ __device__ __host__ inline float math_fn(int fn, float x) {
         default: return 0.0f;
     }
 }
+// Philox blocks for the known-answer tests (ipt_philox): the key arrives as
+// kernel arguments, i.e. uniform, as in the path kernel
+__global__ void philox_kernel(uint32_t k0, uint32_t k1, const uint4* __restrict__ ctr, uint4* __restrict__ out,
+                              long long n) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 c = ctr[i];
+    const u32x4 o = philox4x32_10(c.x, c.y, c.z, c.w, k0, k1);
+    out[i] = make_uint4(o.v[0], o.v[1], o.v[2], o.v[3]);
+}
 __global__ void math_kernel(int fn, const float* in, float* out, long long n) {
     long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = math_fn(fn, in[i]);
@@ -3083,6 +3093,29 @@ int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n
     HIPCHECK(ctx, hipGetLastError());
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHECK(ctx, hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
+    return IPT_OK;
+}
+
+int ipt_philox(ipt_ctx* ctx, uint32_t key0, uint32_t key1, const uint32_t* ctr, uint32_t* out, int64_t n) {
+    if (!ctr || !out || n < 0) return ctx ? fail(ctx, IPT_E_INVALID, "ipt_philox: bad arguments") : IPT_E_INVALID;
+    if (!ctx) {
+        for (int64_t i = 0; i < n; ++i) {
+            const u32x4 o = philox4x32_10(ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3], key0, key1);
+            for (int q = 0; q < 4; ++q) out[4 * i + q] = o.v[q];
+        }
+        return IPT_OK;
+    }
+    hipSetDevice(ctx->device);
+    DevBuf<uint4> din, dout;
+    HIPCHECK(ctx, hipMalloc(&din.p, std::max<int64_t>(n, 1) * sizeof(uint4)));
+    HIPCHECK(ctx, hipMalloc(&dout.p, std::max<int64_t>(n, 1) * sizeof(uint4)));
+    HIPCHECK(ctx, hipMemcpy(din.p, ctr, n * sizeof(uint4), hipMemcpyHostToDevice));
+    if (n > 0)
+        hipLaunchKernelGGL(philox_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, key0, key1,
+                           din.p, dout.p, (long long)n);
+    HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHECK(ctx, hipMemcpy(out, dout.p, n * sizeof(uint4), hipMemcpyDeviceToHost));
     return IPT_OK;
 }
 
