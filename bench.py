@@ -1,18 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X path-tracing inner loop (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): sample_scenes[0] (make_scene_box), 1024^2,
-256 spp, n_rays 16, depth_max 8, fp32, synthetic = the scene itself.
-A *step* renders `--spp-per-step` sample passes of the whole frame (one
-ipt_render_device call: raygen + path kernel + GridRenderPlane accumulate
-kernel); the default step is the full 256-spp frame, rendered by one
-path-kernel launch.
+Workload (BASELINE.json configs[1], the default): sample_scenes[0]
+(make_scene_box), 1024^2, 256 spp, n_rays 16, depth_max 8, fp32, synthetic =
+the scene itself. A *step* renders `--spp-per-step` sample passes of the
+frame (one ipt_render_device call: raygen + path kernel + GridRenderPlane
+accumulate kernel); the default c2 step is the full 256-spp frame, rendered
+by one path-kernel launch.
 
 Multi-GPU (torchrun, one rank per GPU): the frame's destination rows are cut
-into 16-row tiles dealt round-robin to the ranks (weak scaling: the frame is
-1024 x 1024*N so each rank keeps the 1-GPU workload); the path needs no
-data-path collective, and the finished frame is assembled on rank 0 by one
-RCCL reduce per GridRenderPlane buffer at the end of the timed region.
+into 16-row tiles dealt round-robin to the ranks (ipt_params.tile_rows /
+n_shards / shard_id); the path needs no data-path collective. The finished
+frame is assembled on rank 0 at the end of the timed region by ONE gather of
+each rank's owned rows (16 B per owned pixel: GridRenderPlane pixels,
+counters, sums, max), scattered into place on rank 0.
+  --scaling weak   (c1, c2 default): the frame stays W x H and every rank
+                   renders its tiles at N x spp-per-step passes per step, so
+                   the per-rank work is the 1-GPU workload ("1024^2 x N-spp");
+  --scaling strong (c3, c4, c5 default): the frame and its passes are fixed
+                   (C4: 4096^2, C5: 2048^2) and split over the ranks.
+Either way the ranks render disjoint tiles of one frame, so the tile load
+imbalance shows in `ranks` (per-rank path-kernel ms and path counts).
+
+--config c1 is BASELINE.json configs[0], the reference's CPU-runnable case
+(256^2, 16 spp, 4 bounces): the GPU renders it and the CPU baseline leg runs
+the WHOLE C1 frame on the oracle (the C1 plumbing number).
 
 Prints ONE JSON line on rank 0.
 """
@@ -30,48 +42,57 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-
-# BASELINE.json configs: (scene, width, per-rank height, spp per step, steps).
-# A step is one ipt_render_device call: c2's step is the whole 1024^2 x 256 spp
-# frame (one launch of 268 M paths); c3/c5 sample their full spp counts with
-# calls of 16.8 M / 134 M paths. The persistent kernel's end-of-launch tail
-# (lanes out of work while the longest paths finish) is then a small share of
-# the launch, as in the full job.
+# BASELINE.json configs: scene, width, height, spp per step, steps, depth_max,
+# default scaling, CPU-baseline sample (row stride, column stride) per call.
+# c2's step is the whole 1024^2 x 256 spp frame (one launch of 268 M paths);
+# c3/c4/c5 sample their full spp counts with calls of 16.8 M / 537 M / 268 M
+# paths, so that the persistent kernel's end-of-launch tail (lanes out of
+# work while the longest paths finish) stays a small share of each launch.
 CONFIGS = {
-    "c2": ("box", 1024, 1024, 256, 2),      # configs[1]: 1024^2, 256 spp, 8 bounces (the metric)
-    "c3": ("spheres10k", 1024, 1024, 16, 2),  # configs[2]: 10k spheres (64 spp in full; sampled)
-    "c4": ("box", 4096, 4096, 8, 4),         # configs[3]: 4096^2 tiles across GPUs (1024 spp in full)
-    "c5": ("lights256", 2048, 2048, 32, 2),  # configs[4]: 256 emitters, 2048^2 (512 spp in full)
+    "c1": ("box", 256, 256, 16, 1, 4, "weak", None),                 # configs[0]: CPU plumbing case
+    "c2": ("box", 1024, 1024, 256, 2, 8, "weak", (64, 1)),           # configs[1]: the metric
+    "c3": ("spheres10k", 1024, 1024, 16, 2, 8, "strong", (128, 64)),  # configs[2]: 10k spheres (64 spp in full)
+    "c4": ("box", 4096, 4096, 32, 2, 8, "strong", (256, 4)),         # configs[3]: 4096^2 tiles (1024 spp in full)
+    "c5": ("lights256", 2048, 2048, 64, 2, 8, "strong", (128, 16)),  # configs[4]: 256 emitters (512 spp in full)
 }
+METRIC = "Mpaths/sec at 1024^2, 8-bounce, sample_scenes[0]; achieved HBM GB/s"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
-                    help="BASELINE.json workload: c2 (default, the metric's config), c3 10k "
-                         "spheres, c4 4096^2 multi-GPU, c5 256 emitters")
+                    help="BASELINE.json workload: c2 (default, the metric's config), c1 the CPU plumbing "
+                         "case, c3 10k spheres, c4 4096^2 multi-GPU, c5 256 emitters")
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--spp-per-step", type=int, default=None)
     ap.add_argument("--width", type=int, default=None)
-    ap.add_argument("--height", type=int, default=None, help="per-rank share of frame rows")
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None)
     ap.add_argument("--n-rays", type=int, default=16)
-    ap.add_argument("--depth-max", type=int, default=8)
+    ap.add_argument("--depth-max", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20241223)
     ap.add_argument("--tile-rows", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target duration of the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0,
+                    help="minimum duration of the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = this process's CPU share, see cpu_threads())")
     ap.add_argument("--no-counters", action="store_true",
                     help="skip the (untimed) counting re-render used for the roofline")
+    ap.add_argument("--verify", action="store_true",
+                    help="N>1: rank 0 re-renders the whole frame unsharded after the timing and "
+                         "compares it bit for bit with the assembled one")
     a = ap.parse_args()
-    scene, w, h, spp, steps = CONFIGS[a.config]
+    scene, w, h, spp, steps, depth, scaling, cpu_sample = CONFIGS[a.config]
     a.scene = scene
     a.width = a.width or w
     a.height = a.height or h
     a.spp_per_step = a.spp_per_step or spp
     a.steps = a.steps or steps
+    a.depth_max = depth if a.depth_max is None else a.depth_max
+    a.scaling = a.scaling or scaling
+    a.cpu_sample = cpu_sample
     return a
 
 
@@ -87,8 +108,34 @@ def make_desc(name):
     raise ValueError(name)
 
 
+def cpu_threads(requested: int = 0) -> int:
+    """Threads of the CPU baseline: this process's CPU affinity, capped at the
+    job's CPU share (OMP_NUM_THREADS: 16 per GPU on the GPU box, where
+    os.cpu_count() shows the whole machine)."""
+    if requested > 0:
+        return requested
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, desc):
-    """Oracle restatement timed on host cores over a strided row sample."""
+    """The oracle (oracle/ipt_oracle.cpp, the recursive CPU restatement of the
+    reference estimator with glibc libm) timed on this host's cores over a
+    bounded sample of the same workload: strided source pixels of successive
+    passes, at least args.cpu_seconds of wall time (c1: the whole frame)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import ctypes as C
 
@@ -96,38 +143,54 @@ def cpu_baseline(args, desc):
     from ipt_amd import capi
 
     lib = oracle_binding.load()
-    lib.ipt_oracle_render_rows.argtypes = [C.POINTER(capi.Scene), C.POINTER(capi.Params), C.c_int,
-                                           C.c_int, C.c_int, C.POINTER(C.c_uint64)]
-    lib.ipt_oracle_render_rows.restype = C.c_double
+    lib.ipt_oracle_render_rows_values.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                  C.c_int, C.c_void_p]
     s, keep = capi.make_scene(desc)
-    W = args.width
-    H = args.height
-    threads = args.cpu_threads
-    row_step = 64  # 16 rows of the 1024-row frame per phase
-    total_paths = 0
+    W, H = args.width, args.height
+    threads = cpu_threads(args.cpu_threads)
+    total = 0
+    calls = 0
     t0 = time.perf_counter()
-    phase = 0
-    while True:
-        p = capi.make_params(W, H, 1, spp_offset=phase // row_step, n_rays=args.n_rays,
-                             depth_max=args.depth_max, seed=args.seed)
-        n = C.c_uint64()
-        lib.ipt_oracle_render_rows(C.byref(s), C.byref(p), row_step, phase % row_step, threads,
-                                   C.byref(n))
-        total_paths += n.value
-        phase += 37  # co-prime stride over row phases: an unbiased row sample
+    if args.cpu_sample is None:  # c1: the whole C1 frame, all its passes
+        p = capi.make_params(W, H, args.spp_per_step * args.steps, n_rays=args.n_rays, depth_max=args.depth_max,
+                             seed=args.seed)
+        vals = np.zeros(p.spp * W * H, np.float32)
+        rc = lib.ipt_oracle_render_rows_values(C.addressof(s), C.addressof(p), 1, 0, 1, 0, threads, vals.ctypes.data)
+        assert rc == 0
+        total = p.spp * W * H
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    rows = (phase // 37)
+        sample = (f"the whole C1 workload: {W}x{H} x {p.spp} spp = {total} paths in {el:.1f} s")
+    else:
+        rs, cs = args.cpu_sample
+        nr, nc = (H + rs - 1) // rs, (W + cs - 1) // cs
+        vals = np.zeros(nr * nc, np.float32)
+        while True:
+            # call k: rows (37k mod rs) (mod rs), columns (11k mod cs) (mod cs)
+            # of pass k: co-prime strides walk every row and column phase
+            p = capi.make_params(W, H, 1, spp_offset=calls, n_rays=args.n_rays, depth_max=args.depth_max,
+                                 seed=args.seed)
+            rp, cp = (37 * calls) % rs, (11 * calls) % cs
+            rc = lib.ipt_oracle_render_rows_values(C.addressof(s), C.addressof(p), rs, rp, cs, cp, threads,
+                                                   vals.ctypes.data)
+            assert rc == 0
+            total += len(range(rp, H, rs)) * len(range(cp, W, cs))
+            calls += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds:
+                break
+        sample = (f"{calls} calls, each the source pixels at row stride {rs} and column stride {cs} of one "
+                  f"pass (phases 37k mod {rs}, 11k mod {cs}) of the {W}x{H} frame: {total} paths in {el:.1f} s")
     return {
-        "value": total_paths / el / 1e6,
+        "value": total / el / 1e6,
         "unit": "Mpaths/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{rows} x 16 source rows of the {W}x{H} frame (1 pass each, rows strided "
-                   f"by 64 at phases 37k mod 64), {total_paths} paths in {el:.1f} s, "
-                   f"{threads} threads; oracle/ipt_oracle.cpp (recursive CPU restatement, "
-                   f"glibc libm)"),
+        "sample": sample + (f"; {threads} threads (this process's CPU share); oracle/ipt_oracle.cpp, the "
+                            f"recursive CPU restatement of main.cpp:98-184 with glibc libm (the reference's "
+                            f"estimator TUs need boost and cannot be built here, DESIGN.md §2)"),
+        "cpu_model": cpu_model(),
+        "host_cpus": os.cpu_count(),
+        "paths_per_s_per_core": total / el / threads,
     }
 
 
@@ -138,9 +201,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
+    if world != args.gpus and rank == 0:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
     dist = None
     # IPT_BENCH_SHARE_GPU=1 (rehearsal only): every rank on cuda:0, frame-end
     # collectives over gloo on host copies, so the N>1 path runs on a 1-GPU box
@@ -157,43 +219,46 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    def coll(fn, t, *a, **kw):  # collective on a device tensor (host copy under gloo)
-        if not share:
-            return fn(t, *a, **kw)
-        h = t.cpu()
-        fn(h, *a, **kw)
-        t.copy_(h)
-
-    from ipt_amd import capi, roofline, scenes
+    from ipt_amd import capi, roofline, tiles
 
     desc = make_desc(args.scene)
     ctx = capi.Context(local_rank)
     ctx.upload_scene(desc)
 
-    W = args.width
-    H = args.height * world  # weak scaling: the frame grows with the rank count
+    W, H = args.width, args.height
     npix = W * H
-    pixels = torch.zeros(npix, dtype=torch.float32, device=dev)
-    counters = torch.zeros(npix, dtype=torch.int32, device=dev)
-    sums = torch.zeros(npix, dtype=torch.float32, device=dev)
-    pmax = torch.zeros(npix, dtype=torch.float32, device=dev)
+    weak = args.scaling == "weak"
+    spp_step = args.spp_per_step * (world if weak else 1)  # passes of the frame per step
+    # GridRenderPlane state [field][H][W]: pixels, counters, sums, pixel_max
+    state = torch.zeros(4, H, W, dtype=torch.float32, device=dev)
+    pixels, counters, sums, pmax = state[0], state[1].view(torch.int32), state[2], state[3]
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def params(spp, off, flags=0):
-        return capi.make_params(W, H, spp, spp_offset=off, n_rays=args.n_rays,
-                                depth_max=args.depth_max, seed=args.seed,
-                                tile_rows=args.tile_rows if world > 1 else 0, n_shards=world,
-                                shard_id=rank, flags=flags)
+    def params(spp, off, shard=rank, flags=0, n_shards=world):
+        return capi.make_params(W, H, spp, spp_offset=off, n_rays=args.n_rays, depth_max=args.depth_max,
+                                seed=args.seed, tile_rows=args.tile_rows if n_shards > 1 else 0,
+                                n_shards=n_shards, shard_id=shard, flags=flags)
 
-    def render(p):
-        ctx.render_device(p, pixels.data_ptr(), counters.data_ptr(), sums.data_ptr(),
-                          pmax.data_ptr(), stream)
+    def render(p, st=state):
+        ctx.render_device(p, st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr(), stream)
+
+    # the tile plan of every rank (host-only, deterministic): owned rows
+    owned_rows = tiles.owned_rows(W, H, args.tile_rows, world)
+    max_own = max(len(o) for o in owned_rows)
+
+    def host_coll(fn, t, **kw):
+        """A collective on a small host tensor (through the device under RCCL)."""
+        if share:
+            fn(t, **kw)
+            return t
+        d = t.to(dev)
+        fn(d, **kw)
+        return d.cpu()
 
     # warmup (separate passes, then reset the image)
     for i in range(args.warmup):
-        render(params(args.spp_per_step, 1_000_000 + i * args.spp_per_step))
-    for t in (pixels, counters, sums, pmax):
-        t.zero_()
+        render(params(spp_step, 1_000_000 + i * spp_step))
+    state.zero_()
     torch.cuda.synchronize(dev)
 
     if dist:
@@ -202,74 +267,93 @@ def main():
     t0 = time.perf_counter()
     path_ms = acc_ms = 0.0
     for step in range(args.steps):
-        render(params(args.spp_per_step, step * args.spp_per_step))
+        render(params(spp_step, step * spp_step))
         pm, am = ctx.last_kernel_ms()
         path_ms += pm
         acc_ms += am
     if dist:
-        # frame end: assemble the GridRenderPlane on rank 0 (each pixel is owned
-        # by exactly one rank, the others hold zeros)
-        coll(dist.reduce, pixels, 0, op=dist.ReduceOp.SUM)
-        coll(dist.reduce, counters, 0, op=dist.ReduceOp.SUM)
-        coll(dist.reduce, sums, 0, op=dist.ReduceOp.SUM)
-        coll(dist.reduce, pmax, 0, op=dist.ReduceOp.MAX)
+        tiles.assemble(dist, state, owned_rows, rank, host=share)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    my_path_ms = path_ms
     if dist:
-        tt = torch.tensor([elapsed, path_ms, acc_ms], dtype=torch.float64, device=dev)
-        coll(dist.all_reduce, tt, op=dist.ReduceOp.MAX)
-        elapsed, path_ms, acc_ms = tt.tolist()
+        tt = torch.tensor([elapsed, path_ms, acc_ms], dtype=torch.float64)
+        elapsed, path_ms, acc_ms = host_coll(dist.all_reduce, tt, op=dist.ReduceOp.MAX).tolist()
 
-    spp_total = args.steps * args.spp_per_step
+    spp_total = args.steps * spp_step
     total_paths = W * H * spp_total
     value = total_paths / elapsed / 1e6
+
+    verify = None
+    if args.verify and world > 1 and rank == 0:
+        whole = torch.zeros_like(state)
+        for step in range(args.steps):
+            render(params(spp_step, step * spp_step, shard=0, n_shards=1), whole)
+        torch.cuda.synchronize(dev)
+        verify = bool(torch.equal(whole.view(torch.int32), state.view(torch.int32)))
+        del whole
+    mean_pixel = float(pixels.mean().item())
 
     # algorithmic op count of the timed work: re-render the same passes with
     # the kernel's event counters (untimed; counts are deterministic)
     roof = None
     cnt = None
+    ranks = None
     if not args.no_counters:
-        sv = [t.clone() for t in (pixels, counters, sums, pmax)]
+        sv = state.clone()
         ctx.reset_counters()
         for step in range(args.steps):
-            render(params(args.spp_per_step, step * args.spp_per_step, capi.IPT_FLAG_COUNTERS))
+            render(params(spp_step, step * spp_step, flags=capi.IPT_FLAG_COUNTERS))
         torch.cuda.synchronize(dev)
         cnt = ctx.counters()
-        for t, s in zip((pixels, counters, sums, pmax), sv):
-            t.copy_(s)
+        state.copy_(sv)
+        del sv
+        mine = [my_path_ms, cnt["paths"], cnt["traced_rays"]]
         if dist:
-            ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64, device=dev)
-            coll(dist.all_reduce, ct)
+            # per-rank [path ms, paths, traced rays] as a [world, 3] all-reduce
+            # of one-hot rows (no list collectives needed)
+            allr = torch.zeros(world, 3, dtype=torch.float64)
+            allr[rank] = torch.tensor(mine, dtype=torch.float64)
+            allr = host_coll(dist.all_reduce, allr)
+            ranks = [{"rank": r, "path_ms": allr[r, 0].item(), "paths": int(allr[r, 1].item()),
+                      "traced_rays": int(allr[r, 2].item())} for r in range(world)]
+            ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64)
+            ct = host_coll(dist.all_reduce, ct)
             cnt = dict(zip(capi.COUNTER_NAMES, [int(x) for x in ct.tolist()]))
         ops = roofline.ops_from_counters(cnt, n_spheres=len(desc.get("spheres", [])),
                                          n_lights=len(desc.get("lights", [])))
-        # per launch on one rank: ops/world per launch, average launch duration
+        # per launch on one rank: ops/world per launch, the slowest rank's
+        # average launch duration (raygen + path kernel, HIP events)
         launch_s = path_ms / 1e3 / args.steps
         achieved = ops / world / args.steps / launch_s
-        own_pix = npix // world
-        acc_bytes = roofline.accumulate_bytes(own_pix, args.spp_per_step)
+        acc_bytes = roofline.accumulate_bytes(len(owned_rows[rank]) * W, spp_step)
         acc_launch_s = acc_ms / 1e3 / args.steps
-        traffic = None
-        traffic_src = None
         cos_samples = cnt["iterations"] - cnt["light_samples"]
-        path_alg_bytes = roofline.path_bytes(total_paths // world // args.steps, cos_samples // world // args.steps,
+        paths_launch = total_paths // world // args.steps
+        path_alg_bytes = roofline.path_bytes(paths_launch, cos_samples // world // args.steps,
                                              cnt["sphere_frames"] // world // args.steps)
-        pmc_file = ROOT / "profiles" / "pmc_latest.json"
-        if pmc_file.exists():
+        traffic = traffic_src = occ = None
+        for name in (f"pmc_latest_{args.config}.json",) + (("pmc_latest.json",) if args.config == "c2" else ()):
+            pmc_file = ROOT / "profiles" / name
+            if not pmc_file.exists():
+                continue
             try:
                 pm = json.load(open(pmc_file))
                 c0 = pm.get("config", {})
-                if (c0.get("width") == W and c0.get("height") == args.height
-                        and c0.get("spp_per_step") == args.spp_per_step
-                        and "path_kernel_hbm_bytes_per_launch" in pm):
-                    traffic = pm["path_kernel_hbm_bytes_per_launch"]
-                    traffic_src = f"profiles/{pm['tag']}_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, same config)"
+                if (c0.get("width") == W and c0.get("height") == H and c0.get("spp_per_step") == spp_step
+                        and c0.get("depth_max", args.depth_max) == args.depth_max):
+                    traffic = pm.get("path_kernel_hbm_bytes_per_launch")
+                    occ = pm.get("path_kernel_occupancy")
+                    traffic_src = (f"profiles/{pm['tag']}_summary.json (rocprofv3 --pmc passes of the same "
+                                   f"config at N=1: FETCH_SIZE, WRITE_SIZE; SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE)")
+                    break
             except Exception:
-                traffic = None
+                traffic = occ = None
         hbm_ach = path_alg_bytes / launch_s / 1e9
+        comp_bytes = roofline.compulsory_bytes(paths_launch)
         roof = {
             # BASELINE.json's metric asks for achieved HBM GB/s: the top level is
             # the path kernel's HBM roofline; the resource that actually binds
@@ -283,9 +367,18 @@ def main():
             "traffic_unit": "bytes/launch",
             "traffic_source": traffic_src,
             "measured_GBps": (traffic / launch_s / 1e9) if traffic else None,
-            "kernel": "path_kernel",
-            "bytes_per_path": path_alg_bytes / (total_paths // world // args.steps),
+            "kernel": "raygen_kernel + path_kernel",
+            "bytes_per_path": path_alg_bytes / paths_launch,
+            "compulsory": {
+                "bytes_per_path": roofline.COMPULSORY_BYTES_PER_PATH,
+                "achieved": comp_bytes / launch_s / 1e9,
+                "frac": comp_bytes / launch_s / 1e9 / roofline.HBM_PEAK_GBPS,
+                "note": ("the reference's own traffic: the 4 B radiance + 1 B drift code per path that the "
+                         "GridRenderPlane replay reads back; the top level adds the raygen records and the "
+                         "CosineDdf / frame-table gathers (implementation choices that replace VALU work)"),
+            },
             "launch_ms": launch_s * 1e3,
+            "occupancy": occ,
             "binding": "valu",
             "valu": {
                 "achieved": achieved / 1e12,
@@ -303,16 +396,18 @@ def main():
                                             if cnt["bvh_nodes"] or cnt["light_nodes"]
                                             or roofline.light_lattice(cnt, len(desc.get("lights", [])))
                                             else None),
-            "note": ("hbm: algorithmic bytes of one path launch (5 B radiance + drift code and "
-                     "the 32 B raygen record per path, 4 B CosineDdf r gather per cosine-sampled "
-                     "iteration, 8 B frame-table gather per sphere frame) / HIP-event launch "
-                     "time; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per launch of the same "
-                     "config (random 4-8 byte gathers move 64-byte lines). The kernel is bound "
-                     "by instruction issue (VALU work and the exec-mask bookkeeping of its "
+            "note": ("hbm: bytes of one launch of the per-sample work (raygen_kernel + path_kernel: 5 B "
+                     "radiance + drift code per path, the 32 B raygen record written and read back, 4 B "
+                     "CosineDdf r gather per cosine-sampled iteration, 8 B frame-table gather per sphere "
+                     "frame) / its HIP-event duration (raygen is ~0.2 %); traffic = rocprofv3 "
+                     "FETCH_SIZE+WRITE_SIZE of path_kernel per launch of the same config (random 4-8 byte "
+                     "gathers move 64-byte lines); occupancy = mean resident waves per SIMD from "
+                     "SQ_WAVE_CYCLES (quad-cycles) x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs). The kernel "
+                     "is bound by instruction issue (VALU work and the exec-mask bookkeeping of its "
                      "branches; the gather latency is hidden), DESIGN.md sections 4.3 and 6. valu: "
-                     "algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event "
-                     "counters) / launch time against the VALU issue peak 256CU x 4 SIMD32 x "
-                     "2.4GHz -- the binding resource (no MFMA shape; HBM far from peak)"),
+                     "algorithmic op-eq (SURVEY.md §8d cost table x the kernel's event counters) / launch "
+                     "time against the VALU issue peak 256CU x 4 SIMD32 x 32 lanes x 2.4GHz -- the binding "
+                     "resource (no MFMA shape; HBM far from peak)"),
             "hbm_accumulate": {
                 "kernel": "accumulate_kernel",
                 "bound": "hbm",
@@ -326,7 +421,7 @@ def main():
         }
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.config == "c2":
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
         try:
             cpu = cpu_baseline(args, desc)
         except Exception as e:  # the GPU number stands on its own
@@ -334,7 +429,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "Mpaths/sec at 1024^2, 8-bounce, sample_scenes[0]; achieved HBM GB/s",
+            "metric": METRIC,
             "value": value,
             "unit": "Mpaths/s",
             "n_gpus": world,
@@ -342,7 +437,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (sample_scenes[0] geometry/light/camera, Philox per-path RNG)",
@@ -350,9 +445,12 @@ def main():
                                    f"depth_max {args.depth_max}, n_rays {args.n_rays}",
                        "baseline_config": args.config,
                        "width": W, "height": H, "spp": spp_total,
-                       "spp_per_step": args.spp_per_step, "depth_max": args.depth_max,
+                       "spp_per_step": spp_step, "depth_max": args.depth_max,
                        "n_rays": args.n_rays, "tile_rows": args.tile_rows if world > 1 else 0,
-                       "parallelism": f"tiles{world}"},
+                       "parallelism": f"tiles{world}",
+                       "per_rank": ("the whole frame's tiles dealt round-robin; " +
+                                    (f"{args.spp_per_step} x N passes per step (weak)" if weak
+                                     else "the fixed frame split over the ranks (strong)"))},
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu and "value" in cpu else None,
@@ -360,8 +458,17 @@ def main():
             "mrays_per_s": (value * cnt["traced_rays"] / cnt["paths"]) if cnt else None,
             "events_per_path": ({k: cnt[k] / cnt["paths"] for k in cnt if k != "paths"}
                                 if cnt else None),
-            "mean_pixel": float(pixels.mean().item()),
+            "mean_pixel": mean_pixel,
         }
+        if world > 1:
+            out["ranks"] = ranks
+            if ranks:
+                pm = [r["path_ms"] for r in ranks]
+                out["rank_imbalance"] = max(pm) / (sum(pm) / len(pm))
+            out["frame_end"] = (f"one gather of the owned rows to rank 0: {tiles.payload_bytes(W, owned_rows)} B "
+                                f"({16 * W * max_own} B per rank, 16 B per owned pixel)")
+            if verify is not None:
+                out["verify_whole_frame_bit_exact"] = verify
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

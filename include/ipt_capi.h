@@ -175,9 +175,12 @@ const char* ipt_last_error(ipt_ctx* ctx); /* ctx may be NULL (creation errors) *
  * exact sampling tables once: CosineDdf 192 MiB and, for sphere-in-box scenes,
  * the RotateDdf frame-angle table 1 GiB (freed by ipt_destroy). Work buffers
  * grow to the largest render: 37 B per sample (radiance, drift code, raygen
- * record) in chunks of at most 2^29 samples; a call renders all its passes in
- * as few path-kernel launches as that allows (each launch ends in a tail
- * where lanes have run out of paths, so batch passes per call).
+ * record) in equal chunks of at most 2^29 samples (18.5 GiB) and at most 3/4
+ * of the device memory free at the call (plus the context's own work
+ * buffers), so a context's footprint is <= ~20 GiB and contexts sharing a
+ * device get smaller chunks rather than IPT_E_OOM; a call renders all its
+ * passes in as few path-kernel launches as that allows (each launch ends in
+ * a tail where lanes have run out of paths, so batch passes per call).
  * Environment read here (diagnostics): IPT_LNODES_LDS=0 keeps the light BVH in
  * global memory, IPT_LIGHT_GRID=0 disables the light-lattice lookup (the light
  * BVH is used instead), IPT_BLOCKS_PER_CU caps the path kernel's residency. */
@@ -223,7 +226,8 @@ int ipt_reset_counters(ipt_ctx* ctx);
 int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n);
 
 /* Timing of the most recent render call's kernels (ms, HIP events on the
-   launch stream): [0] = path kernel, [1] = accumulate kernel. */
+   launch stream, summed over its chunks): [0] = the path's per-sample work,
+   raygen_kernel + path_kernel (raygen ~0.2 % of it); [1] = accumulate kernel. */
 int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
 
 /* ---- image post-process on the GPU, bit-exact --------

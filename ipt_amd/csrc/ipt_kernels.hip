@@ -2530,16 +2530,32 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     const int W = p->width, H = p->height;
     const size_t per_pass = (size_t)n_cand * W;
     if (per_pass == 0 || p->spp == 0) return IPT_OK;
-    // chunk passes so that the work buffers stay bounded: 2^29 units = 2 GiB of
-    // radiance + 512 MiB of codes + 16 GiB of raygen records (of 288 GB), in
-    // equal chunks: each launch ends with a tail in which lanes run out of work
-    // (the longest paths finish alone; 7 % of a 32-spp C2 launch), so few large
-    // launches beat many small ones (C2 1024^2 x 256 spp is a single launch)
-    const size_t budget = (size_t)1 << 29;
+    // chunk passes so that the work buffers stay bounded: at most 2^29 units
+    // (37 B each: 2 GiB of radiance + 512 MiB of codes + 16 GiB of raygen
+    // records, of 288 GB), and at most 3/4 of the device memory this context
+    // can still obtain (hipMemGetInfo's free memory plus its own work buffers,
+    // less the sampling tables not yet built), so that contexts sharing a
+    // device split their passes into more launches instead of failing with
+    // IPT_E_OOM. Equal chunks: each launch ends with a tail in which lanes run
+    // out of work (the longest paths finish alone; 7 % of a 32-spp C2 launch),
+    // so few large launches beat many small ones (C2 1024^2 x 256 spp is a
+    // single launch).
+    constexpr size_t kUnitBytes = sizeof(float) + 1 + (IPT_RAYGEN ? 2 * sizeof(uint4) : 0);
+    size_t budget = (size_t)1 << 29;
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            size_t avail = free_b + ctx->work_cap * kUnitBytes;
+            const size_t tables = (ctx->d_cos_a ? 0 : ((size_t)3 << 26)) +
+                                  (ctx->d_frame_sc || ctx->geometry_kind != IPT_GEOM_SPHERE_IN_BOX
+                                       ? 0 : kFrameTabEntries * sizeof(float2));
+            avail = avail > tables ? avail - tables : 0;
+            budget = std::min(budget, std::max<size_t>(per_pass, avail / 4 * 3 / kUnitBytes));
+        }
+    }
     const size_t n_chunks = std::max<size_t>(1, ((size_t)p->spp * per_pass + budget - 1) / budget);
     int chunk = (int)std::max<size_t>(1, ((size_t)p->spp + n_chunks - 1) / n_chunks);
     while (chunk > 1 && (size_t)chunk * per_pass > budget) --chunk;
-    if (host_values) chunk = p->spp;  // debug path: one chunk
     int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
     if (rc) return rc;
     rc = ensure_cos_tables(ctx, st);
@@ -2631,11 +2647,13 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.count = count ? 1 : 0;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
+        // ev[0]..ev[1]: the path's per-sample work, raygen_kernel (render_sample's
+        // jitter, camera ray, Philox block 0; ~0.2 % of a C2 launch) and path_kernel
+        HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
         if (IPT_RAYGEN) {
             hipLaunchKernelGGL(raygen_kernel, dim3((unsigned)((kp.total_units + 255) / 256)), dim3(256), 0, st, kp);
             HIPCHECK(ctx, hipGetLastError());
         }
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));  // path kernel alone (raygen is in the call's time)
         if (susp <= 4)
             rc = launch_path<4>(ctx, kp, st, count);
         else if (susp <= 8)
@@ -2666,9 +2684,11 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
             HIPCHECK(ctx, hipGetLastError());
         }
         HIPCHECK(ctx, hipEventRecord(ctx->ev[2], st));
-        if (host_values) {
-            HIPCHECK(ctx, hipMemcpyAsync(host_values, ctx->d_values, sizeof(float) * ns * per_pass, hipMemcpyDeviceToHost, st));
-            HIPCHECK(ctx, hipMemcpyAsync(host_codes, ctx->d_codes, ns * per_pass, hipMemcpyDeviceToHost, st));
+        if (host_values) {  // [spp][H][W] (whole frames: per_pass == W * H)
+            HIPCHECK(ctx, hipMemcpyAsync(host_values + (size_t)s0 * per_pass, ctx->d_values, sizeof(float) * ns * per_pass,
+                                         hipMemcpyDeviceToHost, st));
+            HIPCHECK(ctx, hipMemcpyAsync(host_codes + (size_t)s0 * per_pass, ctx->d_codes, ns * per_pass,
+                                         hipMemcpyDeviceToHost, st));
         }
         HIPCHECK(ctx, hipEventSynchronize(ctx->ev[2]));
         float a = 0, b = 0;
@@ -2753,6 +2773,7 @@ void ipt_destroy(ipt_ctx* ctx) {
 
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!ctx) return IPT_E_INVALID;
+    ctx->has_scene = false;  // any failure below leaves no scene (ipt_capi.h)
     if (!s) return fail(ctx, IPT_E_INVALID, "scene is NULL");
     if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_SMALLPT)
         return fail(ctx, IPT_E_UNSUPPORTED, "unknown geometry_kind");

@@ -96,11 +96,24 @@ def accumulate_bytes(n_dest_pixels: int, spp: int, with_sums: bool = True,
 
 
 def path_bytes(paths: int, cosine_samples: int = 0, frame_builds: int = 0) -> int:
-    """Algorithmic HBM bytes of one path launch, as the kernel moves them: 4 B
-    radiance + 1 B drift code written and the 32 B raygen record read per path,
-    the 4-byte CosineDdf r entry gathered per cosine-sampled iteration (64 MiB
-    table; (cos phi, sin phi) is computed in-lane since round 2), and the 8-byte
-    frame-table entry gathered per sphere-node frame build (1 GiB table; pushes
-    counted, the ~30 % rebuilds after pops are not). Scene data is a few hundred
-    bytes, read once per workgroup."""
-    return (5 + 32) * paths + 4 * cosine_samples + 8 * frame_builds
+    """HBM bytes of one launch of the path's per-sample work (raygen_kernel +
+    path_kernel), as the kernels move them: 4 B radiance + 1 B drift code
+    written per path, the 32 B raygen record written by raygen_kernel and read
+    back by path_kernel, the 4-byte CosineDdf r entry gathered per
+    cosine-sampled iteration (64 MiB table; (cos phi, sin phi) is computed
+    in-lane since round 2), and the 8-byte frame-table entry gathered per
+    sphere-node frame build (1 GiB table; pushes counted, the ~30 % rebuilds
+    after pops are not). Scene data is a few hundred bytes, read once per
+    workgroup. The records and gathers are implementation choices (they
+    replace VALU work); compulsory_bytes() is the reference's own traffic."""
+    return (5 + 2 * 32) * paths + 4 * cosine_samples + 8 * frame_builds
+
+
+# The per-sample output the GridRenderPlane replay needs: the 4-byte radiance
+# and the 1-byte drift code of every path (SURVEY.md §8(d): "compulsory HBM
+# traffic is about 8 B per pixel of output, <= 16 B/path").
+COMPULSORY_BYTES_PER_PATH = 5
+
+
+def compulsory_bytes(paths: int) -> int:
+    return COMPULSORY_BYTES_PER_PATH * paths

@@ -1,12 +1,15 @@
-"""Multi-GPU path on CPU: world_size-2 gloo run of the shard plan + frame-end
-assembly that bench.py performs over RCCL.
+"""Multi-rank path: world_size-2 gloo runs of the tile plan
+and the frame-end assembly (ipt_amd/tiles.py, the code bench.py runs over
+RCCL).
 
-Each rank takes its tile plan from the product (ipt_shard_plan), forms the
-GridRenderPlane rows it owns (here from the oracle; on the GPU box
-test_gpu_parity.py::test_sharded_render_matches_whole_frame checks the
-kernel's shard image equals exactly this), and rank 0 assembles the frame with
-reduce(SUM) / reduce(MAX) — the collective bench.py issues. The assembled
-frame must equal the single-rank frame bit-for-bit.
+* test_two_rank_frame_assembly (CPU): each rank takes its tile plan from the
+  product (ipt_shard_plan), forms the GridRenderPlane rows it owns from the
+  oracle's whole frame, and rank 0 assembles with tiles.assemble (one gather
+  of owned rows); the result must equal the single-rank frame bit for bit.
+* test_two_rank_sharded_render_on_gpu (GPU): the same two-rank run with the
+  PRODUCT rendering each shard (both ranks on cuda:0, gloo for the frame
+  end, as bench.py's IPT_BENCH_SHARE_GPU=1 rehearsal): the assembled frame
+  must equal the whole-frame GPU render and the oracle's replay, bit for bit.
 """
 import os
 import socket
@@ -28,22 +31,32 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _setup(rank, world, port):
     import sys
     from pathlib import Path
 
     root = Path(__file__).resolve().parents[1]
     sys.path.insert(0, str(root))
     sys.path.insert(0, str(root / "tests"))
-    import oracle_binding as ob
-    from ipt_amd import capi, scenes
-
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _state_of(img):
+    return torch.from_numpy(np.stack([img[k].view(np.float32) for k in ("pixels", "counters", "sums", "pixel_max")])
+                            .reshape(4, H, W).copy())
+
+
+def _worker_cpu(rank, world, port, q):
+    _setup(rank, world, port)
+    import oracle_binding as ob
+    from ipt_amd import capi, scenes, tiles
+
     try:
+        owned = tiles.owned_rows(W, H, TILE, world)
         p = capi.make_params(W, H, SPP, tile_rows=TILE, n_shards=world, shard_id=rank)
-        owned, cand = capi.shard_plan(p)
+        _, cand = capi.shard_plan(p)
         vals, codes = ob.render_values(scenes.make_scene_box(), capi.make_params(W, H, SPP))
         # every sample that lands in an owned row is traced by this rank
         for s in range(SPP):
@@ -51,38 +64,84 @@ def _worker(rank, world, port, q):
                 yn = max(H - 2 - iy, 0)
                 for ix in range(W):
                     yi = yn + ((int(codes[s, iy, ix]) >> 2) & 3) - 1
-                    if owned[yi]:
+                    if yi in owned[rank]:
                         assert iy in cand, (rank, iy, yi)
-        full = ob.accumulate(vals, codes)
-        mask = np.repeat(owned, W)
-        part = {k: torch.from_numpy(np.where(mask, v, 0).astype(v.dtype).view(
-            np.int32 if v.dtype == np.uint32 else v.dtype)) for k, v in full.items()}
-        dist.reduce(part["pixels"], 0, op=dist.ReduceOp.SUM)
-        dist.reduce(part["counters"], 0, op=dist.ReduceOp.SUM)
-        dist.reduce(part["sums"], 0, op=dist.ReduceOp.SUM)
-        dist.reduce(part["pixel_max"], 0, op=dist.ReduceOp.MAX)
+        full = _state_of(ob.accumulate(vals, codes))
+        mine = torch.zeros_like(full)  # a rank's render writes only its owned rows
+        mine[:, owned[rank]] = full[:, owned[rank]]
+        tiles.assemble(dist, mine, owned, rank, host=True)
         if rank == 0:
-            ok = all(np.array_equal(part[k].numpy().view(np.uint32),
-                                    full[k].view(np.uint32)) for k in full)
-            q.put(ok)
-        own_count = torch.tensor([int(owned.sum())])
-        dist.all_reduce(own_count)
-        if rank == 0:
-            q.put(int(own_count.item()))
+            q.put(bool(torch.equal(mine.view(torch.int32), full.view(torch.int32))))
+            q.put(sorted(np.concatenate(owned).tolist()) == list(range(H)))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_frame_assembly(oracle):
-    world = 2
+def _worker_gpu(rank, world, port, q):
+    _setup(rank, world, port)
+    import oracle_binding as ob
+    from ipt_amd import capi, scenes, tiles
+
+    try:
+        desc = scenes.make_scene_box()
+        owned = tiles.owned_rows(W, H, TILE, world)
+        ctx = capi.Context(0)
+        ctx.upload_scene(desc)
+        dev = torch.device("cuda", 0)
+        state = torch.zeros(4, H, W, dtype=torch.float32, device=dev)
+
+        def render(p, st):
+            ctx.render_device(p, st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr())
+
+        # two calls continue the same running mean, as bench.py's steps do
+        for s0 in (0, SPP):
+            render(capi.make_params(W, H, SPP, spp_offset=s0, tile_rows=TILE, n_shards=world, shard_id=rank), state)
+        torch.cuda.synchronize(dev)
+        others = np.setdiff1d(np.arange(H), owned[rank])
+        wrote_outside = bool(state[:, others].any().item())
+        tiles.assemble(dist, state, owned, rank, host=True)
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            whole = torch.zeros_like(state)
+            for s0 in (0, SPP):
+                render(capi.make_params(W, H, SPP, spp_offset=s0), whole)
+            torch.cuda.synchronize(dev)
+            vals, codes = ob.render_values(desc, capi.make_params(W, H, 2 * SPP))
+            ref = _state_of(ob.accumulate(vals, codes))
+            got = state.cpu()
+            q.put((wrote_outside, bool(torch.equal(got.view(torch.int32), whole.cpu().view(torch.int32))),
+                   bool(torch.equal(got.view(torch.int32), ref.view(torch.int32)))))
+        else:
+            q.put((wrote_outside,))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(target, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
         pr.join(timeout=300)
         assert pr.exitcode == 0
-    assert q.get(timeout=10) is True
-    assert q.get(timeout=10) == H  # every destination row owned exactly once
+    return [q.get(timeout=10) for _ in range(world if target is _worker_gpu else 2)]
+
+
+def test_two_rank_frame_assembly(oracle):
+    equal, partition = _run(_worker_cpu)
+    assert equal is True
+    assert partition is True  # every destination row owned exactly once
+
+
+@pytest.mark.gpu
+def test_two_rank_sharded_render_on_gpu(oracle):
+    res = _run(_worker_gpu)
+    full = [r for r in res if len(r) == 3]
+    assert len(full) == 1
+    assert not any(r[0] for r in res), "a shard wrote outside its rows"
+    assert full[0][1], "assembled frame != whole-frame GPU render"
+    assert full[0][2], "assembled frame != oracle"
