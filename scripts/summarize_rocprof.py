@@ -1,12 +1,26 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 CSV output into profiles/<tag>_summary.json.
+"""Summarise rocprofv3 CSV output into profiles/<tag>_<cfg>_summary.json and
+profiles/pmc_latest_<cfg>.json (read by bench.py for `traffic` / `occupancy`).
 
-usage: summarize_rocprof.py TAG STATS_DIR FETCH_DIR WRITE_DIR BENCH_JSON
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. Per the gfx950 guide
-(MI355X_MICROARCH.md §HBM) FETCH_SIZE under-reports wide coalesced streaming
-reads by 2x; that correction is applied to the accumulate kernel (4 B/lane
-coalesced stream) and reported separately; the path kernel's reads are
-scalar/uncoalesced and left uncorrected (uncalibrated widths).
+usage: summarize_rocprof.py TAG CFG BENCH_JSON STATS_DIR PMC_DIR [PMC_DIR...]
+
+STATS_DIR: a `rocprofv3 --kernel-trace --stats` run; each PMC_DIR: one
+`rocprofv3 --pmc ... --kernel-trace` pass of the same bench command (one
+counter group per pass, MI355X_MICROARCH.md "rocprofv3 PMC slots").
+Per kernel and dispatch, a counter's rows (its dimension instances) are
+summed; the summary holds the mean over dispatches.
+
+Derived for path_kernel:
+* HBM bytes per launch = (FETCH_SIZE + WRITE_SIZE) KiB x 1024. FETCH_SIZE is
+  not doubled: the guide's 2x correction is for wide coalesced streams; the
+  path kernel's reads are 4-16 B gathers and scalar loads (uncalibrated
+  widths, left as measured). The accumulate kernel's 4 B/lane coalesced
+  stream gets the correction, reported separately.
+* occupancy = mean resident waves per SIMD = SQ_WAVE_CYCLES (quad-cycles,
+  summed over all waves) x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs)
+  (GRBM_GUI_ACTIVE is the sum over the 8 XCDs of the cycles the GPU was busy;
+  MI355X_MICROARCH.md "DVFS give-back", "s_memtime tick vs SQ PMC units");
+  also the effective clock GRBM_GUI_ACTIVE / 8 / kernel time.
 """
 import csv
 import glob
@@ -15,52 +29,72 @@ import shutil
 import sys
 from pathlib import Path
 
-tag, stats_dir, fetch_dir, write_dir, bench_json = sys.argv[1:6]
+tag, cfg_name, bench_json, stats_dir, *pmc_dirs = sys.argv[1:]
 out = Path("profiles")
 out.mkdir(exist_ok=True)
+N_XCD, N_SIMD = 8, 256 * 4
 
 
 def short(name):
-    if "path_kernel" in name:
-        return "path_kernel"
-    if "accumulate_kernel" in name:
-        return "accumulate_kernel"
+    for k in ("path_kernel", "accumulate_kernel", "raygen_kernel"):
+        if k in name:
+            return k
     return name[:40]
 
 
 stats = {}
-for f in glob.glob(f"{stats_dir}/*kernel_stats.csv"):
-    shutil.copy(f, out / f"{tag}_kernel_stats.csv")
+for f in glob.glob(f"{stats_dir}/**/*kernel_stats.csv", recursive=True):
+    shutil.copy(f, out / f"{tag}_{cfg_name}_kernel_stats.csv")
     for r in csv.DictReader(open(f)):
         stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                    "pct": float(r["Percentage"])}
 pmc = {}
-for d, cn in ((fetch_dir, "FETCH_SIZE"), (write_dir, "WRITE_SIZE")):
-    for f in glob.glob(f"{d}/*counter_collection.csv"):
+durations = {}
+for d in pmc_dirs:
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         per = {}
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != cn:
-                continue
             k = short(r["Kernel_Name"])
-            per.setdefault(k, {}).setdefault(r["Dispatch_Id"], 0.0)
-            per[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
-        for k, disp in per.items():
+            per.setdefault((k, r["Counter_Name"]), {}).setdefault(r["Dispatch_Id"], 0.0)
+            per[(k, r["Counter_Name"])][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        for (k, cn), disp in per.items():
             vals = list(disp.values())
-            pmc.setdefault(k, {})[cn + "_KiB_per_dispatch"] = sum(vals) / len(vals)
-bench = json.load(open(bench_json))
+            pmc.setdefault(k, {})[cn] = sum(vals) / len(vals)
+    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            durations.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9)
+
+bench = json.loads(open(bench_json).read().strip().splitlines()[-1])
 cfg = bench["config"]
 paths_per_launch = cfg["width"] * cfg["height"] * cfg["spp_per_step"]
-summary = {"tag": tag, "kernel_stats": stats, "pmc": pmc, "config": cfg,
-           "paths_per_launch": paths_per_launch}
+summary = {"tag": tag, "config_name": cfg_name, "kernel_stats": stats, "pmc": pmc, "config": cfg,
+           "paths_per_launch": paths_per_launch, "bench_value": bench.get("value")}
 pk = pmc.get("path_kernel", {})
-if "FETCH_SIZE_KiB_per_dispatch" in pk and "WRITE_SIZE_KiB_per_dispatch" in pk:
-    b = (pk["FETCH_SIZE_KiB_per_dispatch"] + pk["WRITE_SIZE_KiB_per_dispatch"]) * 1024
+if "FETCH_SIZE" in pk and "WRITE_SIZE" in pk:
+    b = (pk["FETCH_SIZE"] + pk["WRITE_SIZE"]) * 1024
     summary["path_kernel_hbm_bytes_per_launch"] = b
     summary["path_kernel_hbm_bytes_per_path"] = b / paths_per_launch
+if "SQ_WAVE_CYCLES" in pk and "GRBM_GUI_ACTIVE" in pk:
+    busy = pk["GRBM_GUI_ACTIVE"] / N_XCD  # GPU-busy cycles of the dispatch
+    summary["path_kernel_occupancy"] = {
+        "waves_per_simd": pk["SQ_WAVE_CYCLES"] * 4 / (busy * N_SIMD),
+        "max_waves_per_simd_by_launch_bounds": None,
+        "source": "SQ_WAVE_CYCLES x 4 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)",
+    }
+    if "SQ_WAVES" in pk:
+        summary["path_kernel_occupancy"]["waves_launched"] = pk["SQ_WAVES"]
+    if durations.get("path_kernel"):
+        t = sum(durations["path_kernel"]) / len(durations["path_kernel"])
+        summary["path_kernel_occupancy"]["effective_clock_GHz"] = busy / t / 1e9
+for key in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
+            "TCC_HIT_sum", "TCC_MISS_sum"):
+    if key in pk:
+        summary.setdefault("path_kernel_per_path", {})[key] = pk[key] / paths_per_launch
 ak = pmc.get("accumulate_kernel", {})
-if "FETCH_SIZE_KiB_per_dispatch" in ak and "WRITE_SIZE_KiB_per_dispatch" in ak:
-    summary["accumulate_hbm_bytes_per_launch_corrected"] = (
-        2 * ak["FETCH_SIZE_KiB_per_dispatch"] + ak["WRITE_SIZE_KiB_per_dispatch"]) * 1024
-json.dump(summary, open(out / f"{tag}_summary.json", "w"), indent=1)
-json.dump(summary, open(out / "pmc_latest.json", "w"), indent=1)
-print(json.dumps(summary, indent=1))
+if "FETCH_SIZE" in ak and "WRITE_SIZE" in ak:
+    summary["accumulate_hbm_bytes_per_launch_corrected"] = (2 * ak["FETCH_SIZE"] + ak["WRITE_SIZE"]) * 1024
+json.dump(summary, open(out / f"{tag}_{cfg_name}_summary.json", "w"), indent=1)
+json.dump(summary, open(out / f"pmc_latest_{cfg_name}.json", "w"), indent=1)
+print(json.dumps({k: summary.get(k) for k in ("tag", "config_name", "path_kernel_hbm_bytes_per_path",
+                                              "path_kernel_occupancy", "path_kernel_per_path")}, indent=1))
