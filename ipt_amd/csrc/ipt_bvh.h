@@ -43,6 +43,7 @@
 #include <functional>
 #include <vector>
 
+#include "ipt_knobs.h"
 #include "ipt_math.h"
 
 namespace ipt {
@@ -190,9 +191,6 @@ inline void bvh_build_spheres(const float* cr, int n, const float cam[3], float 
     }
     *tmargin = (float)(tm * (1.0 + 1e-6)) + 1e-7f;  // rounded up
     std::vector<int> perm;
-#ifndef IPT_BVH_LEAF
-#define IPT_BVH_LEAF 16
-#endif
     bvh_build_boxes(box, IPT_BVH_LEAF, true, kBvhOrders, nodes, perm, nodes_per_order);
     prims.resize(perm.size());
     for (size_t k = 0; k < perm.size(); ++k) {
@@ -230,9 +228,6 @@ struct SphereGrid {
     std::vector<BvhSphere> items;   // per-cell sphere records
 };
 
-#ifndef IPT_GRID_CELLS_PER_SPHERE
-#define IPT_GRID_CELLS_PER_SPHERE 1.5  // C3 sweep: 0.75-12, best 1.5 with a 5-cell budget
-#endif
 inline bool grid_build_spheres(const float* cr, int n, const float cam[3], float B, SphereGrid& g) {
     if (n <= 0) return false;
     std::vector<double> lo(3 * (size_t)n), hi(3 * (size_t)n);
@@ -351,9 +346,6 @@ inline bool bvh_build_lights(int n, const float (*P)[3], const float (*x)[3], co
         }
     }
     std::vector<int> perm;
-#ifndef IPT_LBVH_LEAF
-#define IPT_LBVH_LEAF 2
-#endif
     bvh_build_boxes(box, IPT_LBVH_LEAF, false, 1, nodes, perm, nodes_per_order);
     return true;
 }

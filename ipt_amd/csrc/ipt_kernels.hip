@@ -34,123 +34,14 @@
 #include "ipt_bvh.h"
 #include "ipt_internal.h"
 #include "ipt_path.h"
+#include "ipt_knobs.h"
+#include "ipt_diag.h"
 
 using namespace ipt;
 
 namespace {
 
-#ifndef IPT_BLOCK
-#define IPT_BLOCK 256
-#endif
-constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; -DIPT_BLOCK for experiments)
-
-// Micro-optimisation switches (all exact; 0 restores the plain form, for A/B builds)
-#ifndef IPT_LV
-#define IPT_LV 3  // single light: its P, x, y, n, inv held in VGPRs (bit mask; +3.5 % C2)
-#endif
-#ifndef IPT_LVG
-#define IPT_LVG 1  // sphere grid: its geometry parameters held in VGPRs (+5 % C3)
-#endif
-#ifndef IPT_BFRESOLVE
-#define IPT_BFRESOLVE 1  // resolve's hit/light/expand decision as selects (+1 %)
-#endif
-#ifndef IPT_NL1
-#define IPT_NL1 1  // kLightsOne: the light count is the compile-time constant 1
-#endif
-#ifndef IPT_UDIV32
-#define IPT_UDIV32 1  // work-unit decomposition in 32-bit arithmetic (units < 2^32)
-#endif
-#ifndef IPT_BOXDIV
-#define IPT_BOXDIV 1  // box planes' divisions without range handling (origins within 2^39)
-#endif
-#ifndef IPT_RESUME
-#define IPT_RESUME 1  // sphere-BVH walks bounded per step and resumed in later steps
-#endif
-#ifndef IPT_GRID_BUDGET
-#define IPT_GRID_BUDGET 5  // grid cells per lane per step of a resumable walk (measured: 4-32; 5 with 1.5 cells per sphere)
-#endif
-#ifndef IPT_LPF
-#define IPT_LPF 1  // lattice instances: the picked light's sample fields gathered in the prologue (C5 +2 %)
-#endif
-#ifndef IPT_GRID_PIPE
-#define IPT_GRID_PIPE 1  // resumable grid walk pipelined: next cell's range + IPT_GRID_ITEMS item loads in flight (C3 +11 %)
-#endif
-#ifndef IPT_GRID_ITEMS
-#define IPT_GRID_ITEMS 3  // item loads issued together per inner iteration of the pipelined grid walk (measured 1-4)
-#endif
-#ifndef IPT_SPHERE_GRID
-#define IPT_SPHERE_GRID 1  // uniform grid instead of the BVH for large sphere lists inside the box
-#endif
-#ifndef IPT_RESUME_LIGHTS
-#define IPT_RESUME_LIGHTS 1  // light-BVH walks bounded per step and resumed (many-light scenes)
-#endif
-#ifndef IPT_LWALK_BUDGET
-#define IPT_LWALK_BUDGET 16  // light-BVH nodes per lane per step of a resumable walk
-#endif
-#ifndef IPT_WALK_BUDGET
-#define IPT_WALK_BUDGET 48  // node visits per lane per step of a resumable walk
-#endif
-#ifndef IPT_WHILE_WHILE
-#define IPT_WHILE_WHILE 1  // BVH walks as while-while loops (leaf work outside the node loop)
-#endif
-#ifndef IPT_LENCMP
-#define IPT_LENCMP 1  // length(a) > length(b) decided on the squares when they are far apart
-#endif
-
-// Profiling-only builds (-DIPT_ABL=n, scripts/ablate.sh): phase n is computed a
-// second time on a perturbed input and kept alive, so the wall-time delta is
-// that phase's marginal cost with the path tree unchanged. 0 in the product.
-#ifndef IPT_ABL
-#define IPT_ABL 0
-#endif
-// Profiling-only builds (-DIPT_PROF=1, scripts/prof_phases.sh): per phase, the
-// number of wave executions and of active lanes in them (lane utilisation),
-// read back with ipt_get_profile().
-#ifndef IPT_PROF
-#define IPT_PROF 0
-#endif
-constexpr int kProfPhases = 12;
-#define IPT_PHASE(id)                                  \
-    if (IPT_PROF) {                                    \
-        const uint64_t pm_ = __ballot(1);              \
-        if ((int)(threadIdx.x & 63) == __ffsll((long long)pm_) - 1) { \
-            prof_w[id] += 1u;                          \
-            prof_l[id] += (uint32_t)__popcll(pm_);     \
-        }                                              \
-    }                                                  \
-    if (IPT_MARK_PHASES) {                             \
-        __builtin_amdgcn_sched_barrier(0);             \
-        asm volatile(";@PHASE " #id);                  \
-        __builtin_amdgcn_sched_barrier(0);             \
-    }
-
-// Diagnostic stamp builds (-DIPT_STAMP=1, scripts/prof_phases.sh): wave-cycles
-// (s_memtime) spent since the previous stamp, per step segment; read their
-// SHARES (the stamps' waits forbid overlaps the real kernel has).
-#ifndef IPT_STAMP
-#define IPT_STAMP 0
-#endif
-#ifndef IPT_MARK_PHASES
-#define IPT_MARK_PHASES 0  // asm-listing builds: a ;@PHASE comment at each IPT_PHASE
-#endif
-#ifndef IPT_MARK
-#define IPT_MARK 0  // asm-listing builds: a ;@STAMP comment at each stamp (scripts/seg_insts.py)
-#endif
-constexpr int kStamps = 12;
-#define IPT_STAMP_AT(id)                                                                   \
-    if (IPT_STAMP) {                                                                       \
-        unsigned long long t_;                                                             \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        st_acc[id] += (uint32_t)(t_ - st_last);                                            \
-        st_last = t_;                                                                      \
-    }                                                                                      \
-    if (IPT_MARK) {                                                                        \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-        asm volatile(";@STAMP " #id);                                                      \
-        __builtin_amdgcn_sched_barrier(0);                                                 \
-    }
+constexpr int kBlock = IPT_BLOCK;  // threads per workgroup (4 waves; ipt_knobs.h)
 template <typename T>
 __device__ __forceinline__ void keep_alive(const T& v) {
     const float* p = reinterpret_cast<const float*>(&v);
@@ -209,38 +100,7 @@ struct KParams {
     const float2* __restrict__ frame_sc;  // frame_table_kernel: RotateDdf angle (sin, cos) by to.z
     const uint4* __restrict__ rg;         // IPT_RAYGEN: [total_units][2] raygen_kernel records
     int count;                            // raygen_kernel: accumulate the drift counter
-    float abl_zero;                       // 0.0f; only read by IPT_ABL profiling builds
 };
-
-#ifndef IPT_SETUP_WAIT
-#define IPT_SETUP_WAIT 1  // drain the setup loads before the step loop
-#endif
-#ifndef IPT_FRAME_PF
-#define IPT_FRAME_PF 3  // 3: the next step's frame-table entry gathered at the end of the step
-                        // (0: in the frame pass; gathering it right after the geometry trace,
-                        // or at the step's end with a predicted node, measured slower)
-#endif
-#ifndef IPT_COSB_INLINE
-#define IPT_COSB_INLINE 1  // (cos phi, sin phi) of CosineDdf computed instead of gathered (+11 % C2)
-#endif
-#ifndef IPT_COSB_INLINE_RES
-#define IPT_COSB_INLINE_RES 1  // the same in the resumable (sphere-list, many-light) instances
-#endif
-#ifndef IPT_LIGHT_INR
-#define IPT_LIGHT_INR 1  // ... with the range-free roots / quotients of light_ranges_box
-#endif
-#ifndef IPT_LIGHT_AXIS
-#define IPT_LIGHT_AXIS 1  // axis-aligned single-light instances (kLightsOneA10/A01)
-#endif
-#ifndef IPT_LIGHT_GRID
-#define IPT_LIGHT_GRID 1  // coplanar light lattices by cell lookup (kLightsGridA10/A01)
-#endif
-#ifndef IPT_CDF_LO
-#define IPT_CDF_LO 1  // many lights: the pick's scan started from a 256-bucket table
-#endif
-#ifndef IPT_RAYGEN
-#define IPT_RAYGEN 1  // new paths' camera ray + RNG state precomputed by raygen_kernel
-#endif
 
 // floor(n / d) for 32-bit n, d >= 1 from a double reciprocal: the estimate's
 // error is below (n/d) * 2^-51 < 1/d (n < 2^32), i.e. below the distance of a
@@ -256,7 +116,6 @@ __host__ __device__ inline uint32_t udiv_exact(uint32_t n, uint32_t d, double in
 // x > y(1+2^-20) (y normal) separates the two correctly rounded roots by more
 // than their rounding; only the rare near-ties (or NaN/tiny) take the roots.
 __device__ __forceinline__ bool longer_sq(float x, float y) {
-    if (!IPT_LENCMP) return sqrt_(x) > sqrt_(y);
     const bool far_gt = x > y * 1.000001907f && y >= 1e-30f;  // 1 + 2^-19
     const bool le = x <= y;
     const bool tie = !far_gt && !le;
@@ -274,10 +133,6 @@ __device__ __forceinline__ void vgpr_hold(float& f) { asm volatile("" : "+v"(f))
 __device__ __forceinline__ void vgpr_hold(vec3& v) { vgpr_hold(v.x); vgpr_hold(v.y); vgpr_hold(v.z); }
 __device__ __forceinline__ void vgpr_hold(int& i) { asm volatile("" : "+v"(i)); }
 
-#ifndef IPT_FRAME_INRANGE
-#define IPT_FRAME_INRANGE 1  // +1.4 % C2
-#endif
-
 // The RotateDdf angle's (sin, cos) are functions of to.z alone: an exact
 // table over every float with |to.z| in [2^-8, 1] (frame_table_kernel, 1 GiB),
 // entry ((bits(|z|) - bits(2^-8)) << 1 | sign); other z (|z| < 2^-8, NaN) are
@@ -285,25 +140,11 @@ __device__ __forceinline__ void vgpr_hold(int& i) { asm volatile("" : "+v"(i)); 
 constexpr uint32_t kFrameTabLo = 0x3b800000u;    // 2^-8
 constexpr uint32_t kFrameTabSpan = 0x04000000u;  // bits(1.0) - bits(2^-8)
 constexpr size_t kFrameTabEntries = 2 * ((size_t)kFrameTabSpan + 1);
-#ifndef IPT_FRAME_TAB
-#define IPT_FRAME_TAB 1  // +8.6 % C2
-#endif
-#ifndef IPT_FRAME_FAST_ALL
-#define IPT_FRAME_FAST_ALL 1  // the fast frame build for the sphere-list scenes too
-#endif
-#ifndef IPT_FRAME_FAST
-#define IPT_FRAME_FAST 1  // sphere-in-box frames without glm's zero terms (make_frame_sc_fast)
-#endif
 __device__ __forceinline__ void frame_sc_lookup(const float2* __restrict__ tab, vec3 to, float& s, float& c) {
     const uint32_t u = f2u(to.z), m = u & 0x7fffffffu;
     const bool in = m - kFrameTabLo <= kFrameTabSpan;
     if (in) {
-#ifdef IPT_EXP_FRAME_MASK
-        // timing experiment only (quantised angle): few cache lines touched
-        const float2 e = tab[(((m - kFrameTabLo) << 1) | (u >> 31)) & IPT_EXP_FRAME_MASK];
-#else
         const float2 e = tab[((m - kFrameTabLo) << 1) | (u >> 31)];
-#endif
         s = e.x;
         c = e.y;
     }
@@ -368,7 +209,6 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
     // near-child-first linearisation for this direction octant (ipt_bvh.h)
     const int oct = (int)(f2u(d.x) >> 31) | (int)(f2u(d.y) >> 31) << 1 | (int)(f2u(d.z) >> 31) << 2;
     const BvhNode* __restrict__ nodes = kp.bvh_nodes + (size_t)oct * kp.n_nodes;
-#if IPT_WHILE_WHILE
     // while-while (Aila & Laine 2009): the inner loop only walks nodes until
     // each lane stands on an entered leaf (or is done), so the leaf's sphere
     // tests run with all such lanes together instead of once per wave-iteration
@@ -402,31 +242,6 @@ __device__ __forceinline__ void sphere_bvh_walk(const KParams& kp, vec3 o, vec3 
             }
         }
     }
-#else
-    while (i < kp.n_nodes && budget-- > 0) {
-        const BvhNode nd = nodes[i];
-        if (COUNT) ++c_nodes;
-        const float te = bvh_box_entry(nd, o, inv);
-        // te == inf is a miss; it must not pass when best is inf too (open floor)
-        const bool enter = te != inf_() && te <= best * 1.0001f + 1e-5f + kp.bvh_tmargin;
-        if (enter && nd.leaf >= 0) {
-            const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
-            if (COUNT) c_tests += (uint32_t)cnt;
-            for (int k2 = 0; k2 < cnt; ++k2) {
-                const BvhSphere sp = kp.bvh_prims[first + k2];
-                const float t = sphere_t(sp.r, o - v3(sp.c[0], sp.c[1], sp.c[2]), d);
-                if (isfinite_(t) && gt_1em6(fabs_(t)) &&
-                    (t < best || (t == best && bidx >= 0 && sp.index < bidx))) {
-                    best = t;
-                    bidx = sp.index;
-                }
-            }
-            i = nd.skip;
-        } else {
-            i = enter ? i + 1 : nd.skip;
-        }
-    }
-#endif
 }
 
 // Uniform-grid walk (ipt_bvh.h SphereGrid; exactness argument there). The
@@ -686,11 +501,8 @@ constexpr int kLdsCand = 512;
 // 64 dwords, so a column's 12 words pair into ds_read2st64/ds_write2st64;
 // 2.7 KiB more, still 4 workgroups/CU); the others keep kBlock + 8 so that
 // their light data fits 4 workgroups as well.
-#ifndef IPT_FS_WIDE
-#define IPT_FS_WIDE 1
-#endif
 __host__ __device__ constexpr int frame_stride(int lmode) {
-    return (IPT_FS_WIDE && (lmode == 1 || lmode == 5 || lmode == 6)) ? kBlock + 64 : kBlock + 8;
+    return (lmode == 1 || lmode == 5 || lmode == 6) ? kBlock + 64 : kBlock + 8;
 }
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
     return 12 * (size_t)frame_stride(lmode) +
@@ -712,9 +524,6 @@ __host__ __device__ inline int global_light_prefix_words(int nl, bool grid = fal
 __host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds, bool grid = false) {
     return (size_t)global_light_prefix_words(nl, grid) + 8 * (size_t)n_nodes_lds;
 }
-#ifndef IPT_WAVES_PER_SIMD
-#define IPT_WAVES_PER_SIMD 4
-#endif
 
 // Where the lights live during the step loop (compile time, so that no
 // generic/flat pointer is ever formed: a flat load would make the compiler
@@ -773,9 +582,6 @@ __host__ __device__ constexpr bool resumable_geom(int geom) {
 __host__ __device__ constexpr bool resumable_lights(int lmode, int geom) {
     return IPT_RESUME_LIGHTS && lmode == 3 /* kLightsGlobal */ && !resumable_geom(geom);
 }
-#ifndef IPT_RES_WAVES
-#define IPT_RES_WAVES 3
-#endif
 __host__ __device__ constexpr int waves_per_simd(int geom, int lmode) {
     return (resumable_geom(geom) || resumable_lights(lmode, geom)) ? IPT_RES_WAVES : IPT_WAVES_PER_SIMD;
 }
@@ -793,19 +599,12 @@ struct RayGen {
 __device__ __forceinline__ RayGen new_path_setup(const KParams& kp, unsigned long long unit, bool sharded,
                                                  const int* cand_rows) {
     RayGen g;
-#if IPT_UDIV32
+    // 32-bit arithmetic with double reciprocals (udiv_exact; units < 2^32)
     const uint32_t u32 = (uint32_t)unit;
     const uint32_t s = udiv_exact(u32, kp.per_pass32, kp.inv_per_pass);
     const uint32_t rem = u32 - s * kp.per_pass32;
     const int cand = (int)udiv_exact(rem, (uint32_t)kp.W, kp.inv_w);
     const int ix = (int)(rem - (uint32_t)cand * (uint32_t)kp.W);
-#else
-    const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
-    const unsigned long long s = unit / per_pass;
-    const unsigned long long rem = unit - s * per_pass;
-    const int cand = (int)(rem / (unsigned long long)kp.W);
-    const int ix = (int)(rem - (unsigned long long)cand * kp.W);
-#endif
     const int iy = sharded ? cand_rows[cand] : cand;
     g.rpass = (uint32_t)(kp.spp_offset + (int)s);
     g.rpix = (uint32_t)(iy * kp.W + ix);
@@ -915,9 +714,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     LS.cg = kp.cdf;
     if (one_light(LMODE)) {
         LS.one = kp.lights[0];
-        if (IPT_LV & 1) { vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y); }
-        if (IPT_LV & 2) { vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]); }
-        if (IPT_LV & 4) { vgpr_hold(LS.one.area); vgpr_hold(LS.one.spow); }
+        // held in VGPRs (+3.5 % C2; area and spow stay uniform)
+        vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y);
+        vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]);
         LS.w0 = kp.weights[0];
         LS.c0 = kp.cdf[0];
         LS.c1 = kp.cdf[1];
@@ -945,9 +744,9 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         else return light_sample_dir<LMODE == kLightsAny>(L, o, a, b);
     };
 
-    // the sphere grid walk's parameters (kRes instances)
+    // the sphere grid walk's parameters (kRes instances), held in VGPRs (+5 % C3)
     KParams kg = kp;
-    if (IPT_LVG && resumable_geom(GEOM)) {
+    if (resumable_geom(GEOM)) {
         for (int a = 0; a < 3; ++a) {
             vgpr_hold(kg.grid_g0[a]);
             vgpr_hold(kg.grid_h[a]);
@@ -958,7 +757,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     }
     const int lane = tid & 63;
     const uint64_t lanemask_lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int nl = (IPT_NL1 && one_light(LMODE)) ? 1 : kp.n_lights;
+    const int nl = one_light(LMODE) ? 1 : kp.n_lights;  // a compile-time 1 for one light
     const float w_sdf = kp.weights[nl];
     const unsigned long long per_pass = (unsigned long long)kp.n_cand * (unsigned long long)kp.W;
     // n at every depth is n_rays >> d; when n_rays is a power of two, res/n ==
@@ -969,7 +768,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     // the setup's vector loads (the single light, weights) complete here, so
     // the step loop's waits never drain them (a conservative vmcnt(0) inside
     // the loop would also drain the step's young table gathers)
-    if (IPT_SETUP_WAIT) __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_waitcnt(0);
 
     // wave-local unit pool (uniform)
     unsigned long long pool_next = 0, pool_end = 0;
@@ -1015,15 +814,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     uint32_t c_paths = 0, c_traced = 0, c_surf = 0, c_light = 0, c_exp = 0, c_iter = 0,
              c_lsamp = 0, c_skip = 0, c_sframe = 0, c_ltr = 0, c_drift = 0, c_nodes = 0, c_tests = 0,
              c_lnode = 0, c_ltest = 0;
-    uint32_t prof_w[kProfPhases], prof_l[kProfPhases];
-    uint32_t st_acc[kStamps];
-    unsigned long long st_last = 0;
-    if (IPT_STAMP) {
-        for (int q = 0; q < kStamps; ++q) st_acc[q] = 0u;
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
-    }
-    if (IPT_PROF)
-        for (int q = 0; q < kProfPhases; ++q) prof_w[q] = prof_l[q] = 0u;
+    IPT_DIAG_STATE  // diagnostic builds only (ipt_diag.h)
 
     for (;;) {
         IPT_STAMP_AT(0);  // previous step's tail (resolve, push, stores)
@@ -1141,7 +932,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             }
             return nrm;
         };
-        constexpr bool kFrameInrange = IPT_FRAME_INRANGE && GEOM == IPT_GEOM_SPHERE_IN_BOX;
+        constexpr bool kFrameInrange = GEOM == IPT_GEOM_SPHERE_IN_BOX;  // range-free frame roots / quotients (+1.4 % C2)
         const bool fneed = need_frame && has_path && !fresh && !((kRes || kResL) && tracing);
         IPT_STAMP_AT(3);  // (new path: later in the step)
         // iteration prologue: RNG window, UnionDdf pick (ddf.cpp:142-153) and,
@@ -1164,27 +955,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // instances a lane keeps its prepared iteration while its walk goes on,
         // so there the gathers stay per lane.)
         auto gathers = [&](bool ran) {
-#ifdef IPT_EXP_GATHER_MASK
-            // timing experiment only (quantised samples): the draws' low bits
-            // dropped, so the table reads touch few cache lines
-            gi_a &= IPT_EXP_GATHER_MASK;
-            gi_b &= IPT_EXP_GATHER_MASK;
-#endif
             if constexpr (kRes || kResL) {
                 if (ran && gcos) {
                     tr = kp.cos_a[gi_a];
-                    if (IPT_COSB_INLINE_RES) {
-                        float sp, cp;
-                        sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
-                        cs_c = cp;
-                        cs_s = sp;
-                    } else {
-                        const float2 tb = kp.cos_b[gi_b];
-                        cs_c = tb.x;
-                        cs_s = tb.y;
-                    }
+                    float sp, cp;
+                    sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
+                    cs_c = cp;
+                    cs_s = sp;
                 }
-            } else if (IPT_COSB_INLINE) {
+            } else {
                 if constexpr (grid_lights(LMODE) && IPT_LPF) {
                     constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
                     const LightDev& Ls = kp.lights[(ran && pick >= 0 && pick < nl) ? pick : 0];
@@ -1202,17 +981,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
                 cs_c = cp;
                 cs_s = sp;
-                if (IPT_ABL == 8) {
-                    float sq, cq;
-                    sincosf_small_(two_pi_times(u01(gi_b << 8)) + kp.abl_zero, &sq, &cq);
-                    keep_alive(sq);
-                    keep_alive(cq);
-                }
-            } else {
-                tr = kp.cos_a[gcos ? gi_a : 0u];
-                const float2 tb = kp.cos_b[gcos ? gi_b : 0u];
-                cs_c = tb.x;
-                cs_s = tb.y;
             }
         };
         auto prologue = [&]() {
@@ -1224,11 +992,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             if (need_b) {
                 IPT_PHASE(4);
                 philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
-                if (IPT_ABL == 3) {
-                    uint32_t q0, q1, q2, q3;
-                    philox_fill(q0, q1, q2, q3, blk + 1 + (uint32_t)kp.abl_zero, rpass, rpix, kp.key0, kp.key1);
-                    keep_alive(q0 ^ q1 ^ q2 ^ q3);
-                }
                 need_b = false;
             }
             const uint32_t j = k & 3u;  // = k - 4*blk: the window was shifted above
@@ -1289,74 +1052,55 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             const vec3 nrm = frame_normal();
             IPT_PHASE(5);
             Frame f;
-            if (IPT_ABL == 9) {
-                // profiling only (not the reference's frame): a trig-free basis
-                // with the same third column, i.e. the same sample distribution
-                const vec3 n = normalize(nrm);
-                const float sg = n.z >= 0.0f ? 1.0f : -1.0f;
-                const float a = -1.0f / (sg + n.z), b = n.x * n.y * a;
-                f.m0 = v3(1.0f + sg * n.x * n.x * a, sg * b, -sg * n.x);
-                f.m1 = v3(b, sg + n.y * n.y * a, -n.y);
-                f.m2 = n;
-                f.iz = n;
-            } else {
-                // the sphere-in-box node's normal comes from a point on the
-                // r = 0.5 sphere: every root and quotient of the frame is in the
-                // range-free sequences' range (make_frame<true>)
-                if (IPT_FRAME_TAB && GEOM == IPT_GEOM_SPHERE_IN_BOX) {
-                    // (sphere-list scenes: measured slower with the table's
-                    // gathers in their latency-bound walks)
-                    vec3 to;
-                    float fs = 0.0f, fc = 0.0f;
-                    if (kFramePf == 3) {
-                        // `to` and its frame-table entry, prepared at the end of
-                        // the previous step (pfok: `to` inside the table's range)
-                        to = pto;
-                        fs = pfs;
-                        fc = pfc;
-                        if (__builtin_expect(__any(!pfok), 0))
-                            if (!pfok) {
-                                to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
-                                frame_sc_lookup(kp.frame_sc, to, fs, fc);
-                                keep_alive(fs);  // its wait stays in this rare branch
-                                keep_alive(fc);
-                            }
-                        pfok = false;
-                    } else {
-                        to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
-                        frame_sc_lookup(kp.frame_sc, to, fs, fc);
-                    }
-                    if (kFrameInrange && IPT_FRAME_FAST) {
-                        // without the zero terms; the rare lanes where a term
-                        // could decide a zero's sign take the exact build
-                        bool ok;
-                        f = make_frame_sc_fast(to, fs, fc, ok);
-                        if (IPT_ABL == 10) {
-                            bool ok2;
-                            keep_alive(make_frame_sc_fast(to, fs + kp.abl_zero, fc, ok2));
+            // the sphere-in-box node's normal comes from a point on the r = 0.5
+            // sphere: every root and quotient of the frame is in the range-free
+            // sequences' range (make_frame<true>)
+            if (IPT_FRAME_TAB && GEOM == IPT_GEOM_SPHERE_IN_BOX) {
+                // (sphere-list scenes: measured slower with the table's
+                // gathers in their latency-bound walks)
+                vec3 to;
+                float fs = 0.0f, fc = 0.0f;
+                if (kFramePf == 3) {
+                    // `to` and its frame-table entry, prepared at the end of
+                    // the previous step (pfok: `to` inside the table's range)
+                    to = pto;
+                    fs = pfs;
+                    fc = pfc;
+                    if (__builtin_expect(__any(!pfok), 0))
+                        if (!pfok) {
+                            to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                            frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                            keep_alive(fs);  // its wait stays in this rare branch
+                            keep_alive(fc);
                         }
-                        if (__builtin_expect(__any(!ok), 0))
-                            if (!ok) f = make_frame_sc<kFrameInrange>(to, fs, fc);
-                    } else {
-                        f = make_frame_sc<kFrameInrange>(to, fs, fc);
-                    }
-                } else if (kFrameInrange) {
-                    f = make_frame<true>(normalize_inrange_(nrm));
-                } else if (IPT_FRAME_FAST_ALL) {
-                    // sphere-list scenes: the f64 angle, then the fast build
-                    // (its own range checks; a normalized `to`), exact fallback
-                    const vec3 to = normalize(nrm);
-                    float fs, fc;
-                    frame_angle_sc(to, &fs, &fc);
+                    pfok = false;
+                } else {
+                    to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
+                    frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                }
+                if (kFrameInrange) {
+                    // without the zero terms; the rare lanes where a term
+                    // could decide a zero's sign take the exact build
                     bool ok;
                     f = make_frame_sc_fast(to, fs, fc, ok);
                     if (__builtin_expect(__any(!ok), 0))
-                        if (!ok) f = make_frame_sc<false>(to, fs, fc);
+                        if (!ok) f = make_frame_sc<kFrameInrange>(to, fs, fc);
                 } else {
-                    f = make_frame(normalize(nrm));
+                    f = make_frame_sc<kFrameInrange>(to, fs, fc);
                 }
+            } else if (kFrameInrange) {
+                f = make_frame<true>(normalize_inrange_(nrm));
+            } else {
+                // sphere-list scenes: the f64 angle, then the fast build
+                // (its own range checks; a normalized `to`), exact fallback
+                const vec3 to = normalize(nrm);
+                float fs, fc;
+                frame_angle_sc(to, &fs, &fc);
+                bool ok;
+                f = make_frame_sc_fast(to, fs, fc, ok);
+                if (__builtin_expect(__any(!ok), 0))
+                    if (!ok) f = make_frame_sc<false>(to, fs, fc);
             }
-            if (IPT_ABL == 1) keep_alive(make_frame(normalize(nrm * (1.0f + kp.abl_zero))));
             float* c = lfr + tid;
             c[0 * kFrameStride] = f.m0.x; c[1 * kFrameStride] = f.m0.y; c[2 * kFrameStride] = f.m0.z;
             c[3 * kFrameStride] = f.m1.x; c[4 * kFrameStride] = f.m1.y; c[5 * kFrameStride] = f.m1.z;
@@ -1446,7 +1190,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             fm.m2 = v3(frc[6 * kFrameStride], frc[7 * kFrameStride], frc[8 * kFrameStride]);
             const vec3 cdir = frame_apply(fm, v3(tr * cs_c, tr * cs_s, sqrt_inrange_(u1)));
             const vec3 ldir = lsample(LS.one, tpos, u1, u2);
-            if (IPT_ABL == 7) keep_alive(lsample(LS.one, tpos, u1 + kp.abl_zero, u2));
             const vec3 zero = v3(0, 0, 0);
             dir_bf = pick < nl ? ldir : (pick == nl ? cdir : zero);
         }
@@ -1463,8 +1206,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     dir = light_sample_dir_axf<XA, YA, IPT_LIGHT_INR>(lpP, lpx, lpy, lpn, lptype, tpos, u1, u2);
                 } else
                 dir = lsample(LS.light(pick), tpos, u1, u2);
-                if (IPT_ABL == 7)
-                    keep_alive(light_sample_dir<LMODE == kLightsAny>(LS.light(pick), tpos, u1 + kp.abl_zero, u2));
                 if (COUNT) ++c_lsamp;
             } else if (pick == nl) {
                 Frame fm;
@@ -1498,9 +1239,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             float cv = 0.0f;
             bool push = false;
             vec3 si_pos = v3(0, 0, 0);
-            if (IPT_BFRESOLVE) {
-                // the same decisions as below as selects (the branches only
-                // cost exec-mask bookkeeping in waves that mix outcomes)
+            {
+                // the reference's hit / light / expand decision (main.cpp:100-143)
+                // as selects (the branches only cost exec-mask bookkeeping in
+                // waves that mix outcomes: +1 %)
                 const bool has_si = prim >= 0;
                 if (COUNT && traced) {
                     ++c_traced;
@@ -1513,40 +1255,19 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // longer(si_pos - o, li_pos - o), asked only where both hits exist
                 const bool need = has_li && has_si;
                 bool lg = x > y * 1.000001907f && y >= 1e-30f;
-                if (!IPT_LENCMP) lg = false;
-                const bool tie = need && (!IPT_LENCMP || (!lg && !(x <= y)));
+                const bool tie = need && (!lg && !(x <= y));
                 if (__builtin_expect(__any(tie), 0))
                     if (tie) lg = sqrt_(x) > sqrt_(y);
                 const bool li_wins = has_li && (!has_si || lg);
                 const int nchild = kp.n_rays >> depth;
                 const float zero = 0.0f;
+                // 0/0 for an expanded node without children: the NaN that
+                // poisons the parent (main.cpp:181)
                 const float cv_exp = nchild == 0 ? zero / (float)nchild : 0.0f;
                 cv = li_wins ? (isfinite_(li_pow) ? li_pow : 1.0f) : (has_si ? cv_exp : 0.0f);
                 cv = traced ? cv : 0.0f;
                 push = traced && !li_wins && has_si && nchild != 0;
                 if (COUNT && traced && !li_wins && has_si) ++c_exp;
-            } else if (traced) {
-                const bool has_si = prim >= 0;
-                if (COUNT) {
-                    ++c_traced;
-                    c_surf += has_si ? 1u : 0u;
-                    c_light += has_li ? 1u : 0u;
-                }
-                if (has_si) si_pos = o + d * t;
-                if (has_li && (!has_si || longer(si_pos - o, li_pos - o))) {
-                    cv = isfinite_(li_pow) ? li_pow : 1.0f;
-                } else if (!has_si) {
-                    cv = 0.0f;
-                } else {
-                    if (COUNT) ++c_exp;
-                    const int nchild = kp.n_rays >> depth;
-                    if (nchild == 0) {
-                        const float zero = 0.0f;
-                        cv = zero / (float)nchild;  // 0/0: the NaN that poisons the parent
-                    } else {
-                        push = true;
-                    }
-                }
             }
             if (push) {
                 IPT_PHASE(10);
@@ -1684,11 +1405,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 const LightDev& L = LS.light(l);
                 vec3 hp, hn;
                 const bool h = ltrace(L, ro, rd, &hp, &hn);
-                if (IPT_ABL == 4) {
-                    vec3 hq, hm;
-                    const bool h2 = ltrace(L, ro, rd * (1.0f + kp.abl_zero), &hq, &hm);
-                    keep_alive(lpdf(L, ro, h2, hq, hm));
-                }
                 if (COUNT) ++c_ltest;
                 if (is_iter) lmix += LS.weight(l) * lpdf(L, ro, h, hp, hn);
                 if (h && (!has_li || longer(li_pos - ro, hp - ro))) {
@@ -1740,7 +1456,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 const vec3 inv = v3(safe_rcp(rd.x), safe_rcp(rd.y), safe_rcp(rd.z));
                 auto walk = [&](const BvhNode* __restrict__ lnodes) {
                 int i = 0;
-#if IPT_WHILE_WHILE
                 // while-while: walk to the next entered leaf, then run the
                 // leaf's light steps with every lane that stands on one
                 while (i < kp.n_light_nodes) {
@@ -1761,20 +1476,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                         for (int l = first; l < first + cnt; ++l) light_step(l);
                     }
                 }
-#else
-                while (i < kp.n_light_nodes) {
-                    const BvhNode nd = lnodes[i];
-                    if (COUNT) ++c_lnode;
-                    const bool enter = bvh_box_entry(nd, ro, inv) != inf_();
-                    if (enter && nd.leaf >= 0) {
-                        const int first = nd.leaf & 0xffffff, cnt = nd.leaf >> 24;
-                        for (int l = first; l < first + cnt; ++l) light_step(l);
-                        i = nd.skip;
-                    } else {
-                        i = enter ? i + 1 : nd.skip;
-                    }
-                }
-#endif
                 };
                 if (kp.lnodes_lds)
                     walk(lnodes_lds);
@@ -1818,11 +1519,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if (rdepth < kp.depth_max) {
                     IPT_PHASE(9);
                     t = trace_geometry<COUNT, GEOM>(kp, ro, rd, &prim, c_nodes, c_tests);
-                    if (IPT_ABL == 5) {
-                        int p2;
-                        keep_alive(trace_geometry<false, GEOM>(kp, ro, rd * (1.0f + kp.abl_zero), &p2, c_nodes, c_tests));
-                        keep_alive(p2);
-                    }
                     IPT_STAMP_AT(10);  // mixture value + geometry trace
                 }
                 resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
@@ -1872,16 +1568,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         }
     }
 
-    if (IPT_STAMP && lane == 0)
-        for (int q = 0; q < kStamps; ++q)
-            atomicAdd(&kp.counters[kNumCounters + 2 * kProfPhases + q], (unsigned long long)st_acc[q]);
-    // (each wave-execution of a phase was counted by its lowest active lane)
-    if (IPT_PROF)
-        for (int q = 0; q < kProfPhases; ++q)
-            if (prof_w[q]) {
-                atomicAdd(&kp.counters[kNumCounters + 2 * q], (unsigned long long)prof_w[q]);
-                atomicAdd(&kp.counters[kNumCounters + 2 * q + 1], (unsigned long long)prof_l[q]);
-            }
+    IPT_DIAG_FLUSH(kp.counters, kNumCounters)
     if (COUNT) {
         atomicAdd(&kp.counters[0], (unsigned long long)c_paths);
         atomicAdd(&kp.counters[1], (unsigned long long)c_traced);
@@ -2474,14 +2161,8 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     HIPCHECK(ctx, hipGetLastError());
     return IPT_OK;
 }
-// -DIPT_C2_ONLY=1: experiment builds (scripts/variants.sh) instantiate the
-// sample_scenes[0] kernel alone (seconds to compile); other scenes fail loudly.
-#ifndef IPT_C2_ONLY
-#define IPT_C2_ONLY 0
-#endif
-#ifndef IPT_C2_LMODE
-#define IPT_C2_LMODE kLightsOneA10
-#endif
+// -DIPT_AB_BUILD -DIPT_C2_ONLY=1: experiment builds (scripts/variants.sh)
+// instantiate the sample_scenes[0] kernel alone (ipt_knobs.h).
 template <int MAXSUSP, bool COUNT, int LMODE>
 int launch_path3(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     if constexpr (IPT_C2_ONLY != 0) {

@@ -1,0 +1,104 @@
+// ipt_knobs.h — the path kernel's build-time parameters. Every switch below
+// selects between EXACT forms (bit-identical results; the parity tests pass
+// with either value); the defaults are the measured best. A
+// build that overrides any of them must say so with -DIPT_AB_BUILD (A/B
+// measurement builds, scripts/variants*.sh), so that a stray -D cannot slip
+// into the product library unnoticed.
+#pragma once
+
+#if !defined(IPT_AB_BUILD) &&                                                                           \
+    (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
+     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
+     defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
+     defined(IPT_RES_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
+     defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || \
+     defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
+     defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE))
+#error "an ipt_knobs.h parameter is overridden: A/B builds must define IPT_AB_BUILD"
+#endif
+
+// ---- launch shape
+#ifndef IPT_BLOCK
+#define IPT_BLOCK 256  // threads per workgroup (4 waves; 128 / 512 measured -2 % / -7 %)
+#endif
+#ifndef IPT_WAVES_PER_SIMD
+#define IPT_WAVES_PER_SIMD 4  // __launch_bounds__ occupancy of the non-resumable instances
+#endif
+#ifndef IPT_RES_WAVES
+#define IPT_RES_WAVES 3  // ... of the resumable (sphere-list, many-light BVH) instances
+#endif
+
+// ---- structure (each also has a runtime or scene condition)
+#ifndef IPT_RAYGEN
+#define IPT_RAYGEN 1  // new paths' camera ray + Philox block 0 precomputed by raygen_kernel (+4.8 % C2)
+#endif
+#ifndef IPT_FRAME_TAB
+#define IPT_FRAME_TAB 1  // RotateDdf angle (sin, cos) from the exact 1 GiB frame table (+8.6 % C2)
+#endif
+#ifndef IPT_FRAME_PF
+#define IPT_FRAME_PF 3  // 3: the next step's frame-table entry gathered at the end of the step
+                        // (0: in the frame pass; gathering it right after the geometry trace,
+                        // or at the step's end with a predicted node, measured slower)
+#endif
+#ifndef IPT_BOXDIV
+#define IPT_BOXDIV 1  // box planes' divisions without range handling (origins within 2^39)
+#endif
+#ifndef IPT_LIGHT_AXIS
+#define IPT_LIGHT_AXIS 1  // axis-aligned single-light instances (kLightsOneA10/A01, +1.7 % C2)
+#endif
+#ifndef IPT_LIGHT_INR
+#define IPT_LIGHT_INR 1  // ... with the range-free roots / quotients of light_ranges_box (+4.9 % C2)
+#endif
+#ifndef IPT_LIGHT_GRID
+#define IPT_LIGHT_GRID 1  // coplanar light lattices by cell lookup (kLightsGridA10/A01; C5 3x)
+#endif
+#ifndef IPT_LPF
+#define IPT_LPF 1  // lattice instances: the picked light's sample fields gathered in the prologue (C5 +2 %)
+#endif
+#ifndef IPT_CDF_LO
+#define IPT_CDF_LO 1  // many lights: the pick's scan started from a 256-bucket table (+7 % C5)
+#endif
+#ifndef IPT_SPHERE_GRID
+#define IPT_SPHERE_GRID 1  // uniform grid instead of the BVH for large sphere lists inside the box
+#endif
+#ifndef IPT_RESUME
+#define IPT_RESUME 1  // sphere-list walks bounded per step and resumed in later steps
+#endif
+#ifndef IPT_RESUME_LIGHTS
+#define IPT_RESUME_LIGHTS 1  // light-BVH walks bounded per step and resumed (many-light scenes)
+#endif
+#ifndef IPT_GRID_PIPE
+#define IPT_GRID_PIPE 1  // resumable grid walk pipelined: next cell's range + IPT_GRID_ITEMS loads in flight (C3 +11 %)
+#endif
+
+// ---- walk budgets and acceleration-structure parameters
+#ifndef IPT_GRID_BUDGET
+#define IPT_GRID_BUDGET 5  // grid cells per lane per step of a resumable walk (measured 4-32)
+#endif
+#ifndef IPT_GRID_ITEMS
+#define IPT_GRID_ITEMS 3  // item loads issued together per inner iteration of the pipelined grid walk (1-4)
+#endif
+#ifndef IPT_WALK_BUDGET
+#define IPT_WALK_BUDGET 48  // sphere-BVH node visits per lane per step of a resumable walk
+#endif
+#ifndef IPT_LWALK_BUDGET
+#define IPT_LWALK_BUDGET 16  // light-BVH nodes per lane per step of a resumable walk
+#endif
+#ifndef IPT_BVH_LEAF
+#define IPT_BVH_LEAF 16  // sphere BVH: median split down to this many spheres (ipt_bvh.h)
+#endif
+#ifndef IPT_LBVH_LEAF
+#define IPT_LBVH_LEAF 2  // light BVH leaf size
+#endif
+#ifndef IPT_GRID_CELLS_PER_SPHERE
+#define IPT_GRID_CELLS_PER_SPHERE 1.5  // C3 sweep: 0.75-12, best 1.5 with a 5-cell budget
+#endif
+
+// ---- experiment builds: -DIPT_AB_BUILD -DIPT_C2_ONLY=1 instantiates the
+// sample_scenes[0] kernel alone (seconds to compile); other scenes fail loudly
+#ifndef IPT_C2_ONLY
+#define IPT_C2_ONLY 0
+#endif
+#ifndef IPT_C2_LMODE
+#define IPT_C2_LMODE kLightsOneA10
+#endif

@@ -46,59 +46,13 @@ IPT_HD float inf_() { return u2f(0x7f800000u); }
 IPT_HD double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 IPT_HD double sqrtd_(double x) { return __builtin_sqrt(x); }
 
-// IEEE f32 sqrt and division with the device compiler's own correction
-// sequences, minus their range handling, for waves whose every active lane is
-// inside the range where that handling is the identity:
-//  * sqrtf: hipcc emits scale-by-2^32 below 2^-96, v_sqrt_f32, a +-1-ulp
-//    correction from two fma residuals, unscale, and a class fixup for
-//    +-0/inf/NaN. For finite x >= 2^-96 the scale, unscale and fixup do
-//    nothing, so the correction core alone is bit-identical.
-//  * a/b: hipcc emits v_div_scale (x2), v_rcp_f32, a reciprocal Newton step,
-//    two quotient residual steps, v_div_fmas, v_div_fixup. With |a|, |b| in
-//    [2^-40, 2^41) no operand is scaled (exponent difference < 96, nothing
-//    denormal), v_div_fmas is a plain fma and v_div_fixup passes the normal
-//    quotient through, so the core alone is bit-identical.
-// Both are proven on the device: sqrt over all 2^32 inputs, division over
-// 2^32 in-range pairs plus zero numerators (ipt_math_selfcheck fn 9/10,
-// tests/test_gpu_parity.py).
-// A wave with any lane outside the range takes the compiler's full sequence.
-#ifndef IPT_FAST_SQRT
-#define IPT_FAST_SQRT 0  // measured neutral on C2 (141.3 vs 141.9 Mpaths/s)
-#endif
-#ifndef IPT_FAST_DIV
-#define IPT_FAST_DIV 0  // measured -12 % on C2: the guard + branch cost more than div_scale/fixup
-#endif
-IPT_HD float sqrt_(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && IPT_FAST_SQRT
-    const bool ok = x >= u2f(0x0f800000u) && x < u2f(0x7f800000u);  // [2^-96, inf)
-    if (__builtin_expect(__all(ok), 1)) {
-        const float s = __builtin_amdgcn_sqrtf(x);
-        const float sd = u2f(f2u(s) - 1u), su = u2f(f2u(s) + 1u);
-        const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
-        const float s1 = rd <= 0.0f ? sd : s;
-        return ru > 0.0f ? su : s1;
-    }
-#endif
-    return __builtin_sqrtf(x);
-}
-IPT_HD float div_(float a, float b) {
-#if defined(__HIP_DEVICE_COMPILE__) && IPT_FAST_DIV
-    // biased exponents in [87, 167]: |a|, |b| in [2^-40, 2^41); a may also be
-    // +-0, whose IEEE quotient is the zero with the xor of the signs
-    const uint32_t ua = f2u(a), ub = f2u(b);
-    const bool a_zero = (ua & 0x7fffffffu) == 0u;
-    const bool ok = (((ua >> 23 & 0xffu) - 87u) <= 80u || a_zero) && ((ub >> 23 & 0xffu) - 87u) <= 80u;
-    if (__builtin_expect(__all(ok), 1)) {
-        float y = __builtin_amdgcn_rcpf(b);
-        y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
-        const float q0 = a * y;
-        const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
-        const float q = __builtin_fmaf(__builtin_fmaf(-b, q1, a), y, q1);
-        return a_zero ? u2f((ua ^ ub) & 0x80000000u) : q;
-    }
-#endif
-    return a / b;
-}
+// IEEE f32 sqrt and division: the device compiler's own sequences. (Wave-
+// guarded variants that drop their range handling measured neutral (sqrt) and
+// -12 % (division: the guard and its branch cost more than v_div_scale /
+// v_div_fixup); the range-free cores below are used only where a host or
+// algebraic proof bounds the operands.)
+IPT_HD float sqrt_(float x) { return __builtin_sqrtf(x); }
+IPT_HD float div_(float a, float b) { return a / b; }
 
 // a/b without the range handling of the compiler's sequence (no v_div_scale /
 // v_div_fmas / v_div_fixup): the reciprocal, one Newton step and two quotient

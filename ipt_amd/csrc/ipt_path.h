@@ -42,16 +42,8 @@ struct Frame {
 // (ddf_detail.h:82), a in [0, pi]
 IPT_HD void frame_angle_sc(vec3 to, float* s, float* c) {
     const float cosinus = dot(v3(0.0f, 0.0f, 1.0f), to);
-#if defined(__HIP_DEVICE_COMPILE__) && defined(IPT_ABL) && (IPT_ABL == 11 || IPT_ABL == 13)
-    const float a = acosf(cosinus);  // profiling only: not the reference's rounding
-#else
     const float a = acos_f64_to_f32(cosinus);
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && defined(IPT_ABL) && (IPT_ABL == 12 || IPT_ABL == 13)
-    *s = __sinf(a); *c = __cosf(a);  // profiling only
-#else
     sincosf_small_(a, s, c);
-#endif
 }
 // The frame from `to` and the angle's (s, c) (make_frame below, or an exact
 // table of frame_angle_sc by to.z's bits in the path kernel).
@@ -177,33 +169,19 @@ IPT_HD vec3 cosine_sample_local(float u1, float u2) {
 // 1 - sgn*oa is 0 or in [2^-24, 2^40) (1 - oa is exact near 1) and the divisor
 // in [1e-6, 2): the range-free division is exact (div_inrange_); a zero
 // numerator gives t = +-0, rejected below either way.
-// IPT_BRANCHFREE: the early returns of the plane / sphere / area-light tests
-// become one select over every test (same comparisons, same arithmetic, so
-// the same result for every input incl. NaN); in a wave that mixes passing
-// and failing lanes the branches only cost exec-mask bookkeeping.
-#ifndef IPT_BFPDF
-#define IPT_BFPDF 1  // light_pdf's facing test as a select
-#endif
-#ifndef IPT_BRANCHFREE
-#define IPT_BRANCHFREE 1  // +3.3 % C2
-#endif
+// Branch-free: the reference's early returns (here and in the area-light
+// test and pdf below) are one select over every test (same comparisons, same
+// arithmetic, so the same result for every input incl. NaN); in a wave that
+// mixes passing and failing lanes the branches only cost exec-mask
+// bookkeeping (+3.3 % C2 when introduced).
 template <bool INRANGE = false>
 IPT_HD float box_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
     const float dp = sgn * da;
-    if (IPT_BRANCHFREE) {
-        const float t = INRANGE ? div_inrange_(1.0f - sgn * oa, dp) : div_(1.0f - sgn * oa, dp);
-        const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
-        const bool miss = lt_1em6(fabs_(dp)) | (fabs_(px) > 1.0f) | (fabs_(py) > 1.0f) | (fabs_(pz) > 1.0f) |
-                          (dp < 0.0f) | lt_1em6(t);
-        return miss ? inf_() : t;
-    }
-    if (lt_1em6(fabs_(dp))) return inf_();
     const float t = INRANGE ? div_inrange_(1.0f - sgn * oa, dp) : div_(1.0f - sgn * oa, dp);
     const float px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
-    if (fabs_(px) > 1.0f || fabs_(py) > 1.0f || fabs_(pz) > 1.0f) return inf_();
-    if (dp < 0.0f) return inf_();
-    if (lt_1em6(t)) return inf_();
-    return t;
+    const bool miss = lt_1em6(fabs_(dp)) | (fabs_(px) > 1.0f) | (fabs_(py) > 1.0f) | (fabs_(pz) > 1.0f) |
+                      (dp < 0.0f) | lt_1em6(t);
+    return miss ? inf_() : t;
 }
 
 // intersection_with_sphere (geometric_utils.cpp:28-55). The f64 expression
@@ -271,62 +249,34 @@ IPT_HD float facing_plane_t(float oa, float da, float sgn, vec3 o, vec3 d) {
 // reference's order {+x,+y,+z,-x,-z}, 5 = the r=0.5 sphere.
 template <bool INRANGE = false>
 IPT_HD float trace_box_planes_only(vec3 o, vec3 d, int* prim) {
-    if (IPT_BRANCHFREE) {
-        // a NaN direction fails every test (the reference returns no hit);
-        // the planes are computed regardless and the result selected at the end
-        const bool dnan = d.x + d.y + d.z != d.x + d.y + d.z;
-        const bool xp = d.x > 0.0f, zp = d.z > 0.0f;
-        float best = facing_plane_t<INRANGE>(o.x, d.x, xp ? 1.0f : -1.0f, o, d);
-        int bi = xp ? 0 : 3;
-        const float ty0 = facing_plane_t<INRANGE>(o.y, d.y, 1.0f, o, d);
-        const float ty = d.y > 0.0f ? ty0 : inf_();
-        // the scan's "nearer, or as near with a lower index" as selects (bitwise
-        // on the comparisons: no short-circuit control flow)
-        const bool take_y = (ty < best) | ((ty == best) & (1 < bi) & (ty != inf_()));
-        best = take_y ? ty : best;
-        bi = take_y ? 1 : bi;
-        const float tz = facing_plane_t<INRANGE>(o.z, d.z, zp ? 1.0f : -1.0f, o, d);
-        const int iz = zp ? 2 : 4;
-        const bool take_z = (tz < best) | ((tz == best) & (iz < bi) & (tz != inf_()));
-        best = take_z ? tz : best;
-        bi = take_z ? iz : bi;
-        const bool none = dnan | (best == inf_());
-        *prim = none ? -1 : bi;
-        return dnan ? inf_() : best;
-    }
-    float best = inf_();
-    int bi = -1;
-    if (d.x + d.y + d.z != d.x + d.y + d.z) {  // NaN direction: every test fails
-        *prim = -1;
-        return best;
-    }
+    // a NaN direction fails every test (the reference returns no hit); the
+    // planes are computed regardless and the result selected at the end
+    const bool dnan = d.x + d.y + d.z != d.x + d.y + d.z;
     // x: the facing plane is +x (index 0) for d.x>0 and -x (index 3) otherwise
-    {
-        const float s = d.x > 0.0f ? 1.0f : -1.0f;
-        const float t = box_plane_t<INRANGE>(o.x, d.x, s, o, d);
-        const int i = d.x > 0.0f ? 0 : 3;
-        best = t;
-        bi = i;
-    }
-    {
-        const float t = d.y > 0.0f ? box_plane_t<INRANGE>(o.y, d.y, 1.0f, o, d) : inf_();
-        if (t < best || (t == best && 1 < bi && t != inf_())) { best = t; bi = 1; }
-    }
-    {
-        const float s = d.z > 0.0f ? 1.0f : -1.0f;
-        const float t = box_plane_t<INRANGE>(o.z, d.z, s, o, d);
-        const int i = d.z > 0.0f ? 2 : 4;
-        if (t < best || (t == best && i < bi && t != inf_())) { best = t; bi = i; }
-    }
-    if (best == inf_()) bi = -1;
-    *prim = bi;
-    return best;
+    const bool xp = d.x > 0.0f, zp = d.z > 0.0f;
+    float best = facing_plane_t<INRANGE>(o.x, d.x, xp ? 1.0f : -1.0f, o, d);
+    int bi = xp ? 0 : 3;
+    const float ty0 = facing_plane_t<INRANGE>(o.y, d.y, 1.0f, o, d);
+    const float ty = d.y > 0.0f ? ty0 : inf_();
+    // the scan's "nearer, or as near with a lower index" as selects (bitwise
+    // on the comparisons: no short-circuit control flow)
+    const bool take_y = (ty < best) | ((ty == best) & (1 < bi) & (ty != inf_()));
+    best = take_y ? ty : best;
+    bi = take_y ? 1 : bi;
+    const float tz = facing_plane_t<INRANGE>(o.z, d.z, zp ? 1.0f : -1.0f, o, d);
+    const int iz = zp ? 2 : 4;
+    const bool take_z = (tz < best) | ((tz == best) & (iz < bi) & (tz != inf_()));
+    best = take_z ? tz : best;
+    bi = take_z ? iz : bi;
+    const bool none = dnan | (best == inf_());
+    *prim = none ? -1 : bi;
+    return dnan ? inf_() : best;
 }
 template <bool INRANGE = false>
 IPT_HD float trace_box(vec3 o, vec3 d, int* prim) {
     int bi;
     float best = trace_box_planes_only<INRANGE>(o, d, &bi);
-    const float ts = sphere_t<IPT_BRANCHFREE, INRANGE>(0.5f, o, d);
+    const float ts = sphere_t<true, INRANGE>(0.5f, o, d);
     if (ts < best) { best = ts; bi = 5; }
     *prim = bi;
     return best;
@@ -381,31 +331,14 @@ IPT_HD bool light_trace(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* nrm)
         return true;
     }
     const float n_dir = dot(L.n, d);
-    if (IPT_BRANCHFREE) {
-        const float t = div_(dot(L.n, L.P - o), n_dir);
-        const vec3 rel = (o + d * t) - L.P;
-        const vec3 coord = mul(L.inv, rel);
-        const bool in = L.type == 0
-                            ? (coord.x >= 0.0f) & (coord.x <= 1.0f) & (coord.y >= 0.0f) & (coord.y <= 1.0f)
-                            : (coord.x >= 0.0f) & (coord.y >= 0.0f) & (coord.x + coord.y <= 1.0f);
-        *hit = L.P + rel;
-        *nrm = L.n;
-        return !(lt_1em6(fabs_(n_dir)) | (n_dir > 0.0f)) & !lt_1em6(t) & in;
-    }
-    if (lt_1em6(fabs_(n_dir)) || n_dir > 0.0f) return false;
     const float t = div_(dot(L.n, L.P - o), n_dir);
-    if (lt_1em6(t)) return false;
     const vec3 rel = (o + d * t) - L.P;
     const vec3 coord = mul(L.inv, rel);
-    bool h;
-    if (L.type == 0)
-        h = coord.x >= 0.0f && coord.x <= 1.0f && coord.y >= 0.0f && coord.y <= 1.0f;
-    else
-        h = coord.x >= 0.0f && coord.y >= 0.0f && coord.x + coord.y <= 1.0f;
-    if (!h) return false;
+    const bool in = L.type == 0 ? (coord.x >= 0.0f) & (coord.x <= 1.0f) & (coord.y >= 0.0f) & (coord.y <= 1.0f)
+                                : (coord.x >= 0.0f) & (coord.y >= 0.0f) & (coord.x + coord.y <= 1.0f);
     *hit = L.P + rel;
     *nrm = L.n;
-    return true;
+    return !(lt_1em6(fabs_(n_dir)) | (n_dir > 0.0f)) & !lt_1em6(t) & in;
 }
 
 // DdfFromLight::value for a direction whose light trace is `has`/`hit`/`nrm`
@@ -414,16 +347,10 @@ IPT_HD float light_pdf(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nrm) 
     if (!has) return 0.0f;
     const vec3 dir = normalize(hit - o);
     const float cosinus = dot(nrm, -dir);
-    if (IPT_BFPDF) {
-        const vec3 ho = hit - o;
-        const float decay = dot(ho, ho);
-        const float p = div_(div_(decay, cosinus), L.area);
-        return cosinus < 0.0f ? 0.0f : p;
-    }
-    if (cosinus < 0.0f) return 0.0f;
     const vec3 ho = hit - o;
     const float decay = dot(ho, ho);
-    return div_(div_(decay, cosinus), L.area);
+    const float p = div_(div_(decay, cosinus), L.area);
+    return cosinus < 0.0f ? 0.0f : p;  // the facing test as a select
 }
 
 // DdfFromLight::sample (lighting.cpp:125-134) via Light::sample:

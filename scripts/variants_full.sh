@@ -7,7 +7,7 @@ mkdir -p ipt_amd/lib/abl
 while [ $# -ge 2 ]; do
   n=$1; f=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
-    -Wno-unused-value $f -o ipt_amd/lib/abl/libipt_$n.so ipt_amd/csrc/ipt_kernels.hip ipt_amd/csrc/ipt_post.hip &
+    -Wno-unused-value -DIPT_AB_BUILD $f -o ipt_amd/lib/abl/libipt_$n.so ipt_amd/csrc/ipt_kernels.hip ipt_amd/csrc/ipt_post.hip &
   pids="$pids $!"
 done
 for p in $pids; do wait $p || { echo "variant build failed"; exit 1; }; done
