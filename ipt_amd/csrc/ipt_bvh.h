@@ -228,6 +228,33 @@ struct SphereGrid {
     std::vector<BvhSphere> items;   // per-cell sphere records
 };
 
+// A grid cell with its first three items inline (64 bytes, one cache line):
+// the walk's next cell is known from the DDA alone, so its record -- item
+// range and first items -- is fetched one cell ahead in a single round trip
+// instead of the range, then the items. Items beyond the third are read from
+// SphereGrid::items[s0 + 3, s1) as before; it[q] copies items[s0 + q].c / r.
+struct GridCell {
+    int s0, s1, pad0, pad1;
+    float it[3][4];
+};
+static_assert(sizeof(GridCell) == 64, "GridCell is one 64-byte line");
+inline void grid_cells_build(const SphereGrid& g, std::vector<GridCell>& cells) {
+    const size_t nc = g.start.size() - 1;
+    cells.assign(nc, GridCell{});
+    for (size_t c = 0; c < nc; ++c) {
+        GridCell& r = cells[c];
+        r.s0 = g.start[c];
+        r.s1 = g.start[c + 1];
+        for (int q = 0; q < 3 && r.s0 + q < r.s1; ++q) {
+            const BvhSphere& b = g.items[(size_t)r.s0 + q];
+            r.it[q][0] = b.c[0];
+            r.it[q][1] = b.c[1];
+            r.it[q][2] = b.c[2];
+            r.it[q][3] = b.r;
+        }
+    }
+}
+
 inline bool grid_build_spheres(const float* cr, int n, const float cam[3], float B, SphereGrid& g) {
     if (n <= 0) return false;
     std::vector<double> lo(3 * (size_t)n), hi(3 * (size_t)n);

@@ -77,6 +77,7 @@ struct KParams {
     float grid_g0[3], grid_h[3], grid_inv_h[3], grid_m;
     int grid_n[3];
     const int* __restrict__ grid_start;   // [cells + 1]
+    const GridCell* __restrict__ grid_cells;  // [cells] range + first three items (IPT_GRID_INLINE)
     const BvhSphere* __restrict__ grid_items;
     const BvhNode* __restrict__ bvh_nodes;     // n_nodes > 0: sphere BVH (ipt_bvh.h)
     const BvhSphere* __restrict__ bvh_prims;
@@ -288,7 +289,98 @@ template <bool COUNT, bool POS = false>
 __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3 d, int& cell, vec3& tmx, float& best,
                                                  int& bidx, int budget, uint32_t& c_nodes, uint32_t& c_tests) {
     const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
-    if constexpr (POS) {
+    auto accept = [&](float t, int k2) {  // FractalSpheres.cpp:75-84's rule on item positions
+        if (isfinite_(t) && gt_1em6(fabs_(t))) {
+            if (t < best)
+                bidx = k2;
+            else if (t == best && bidx >= 0 && kp.grid_items[k2].index < kp.grid_items[bidx].index)
+                bidx = k2;
+            best = t < best ? t : best;
+        }
+    };
+    if constexpr (POS && IPT_GRID_INLINE) {
+        // cells as 64-byte records (GridCell: the item range and the first
+        // three items): the next cell follows from tmx alone, so its record is
+        // fetched while the current cell's items are tested -- one round trip
+        // per cell, overlapped, instead of a range load and then item loads.
+        // Same cells, items, tests and exit decisions as the walk below.
+        if (cell < 0 || budget <= 0) return;
+        auto lin_of = [&](int c) {
+            return (c & 0xff) + kp.grid_n[0] * (((c >> 8) & 0xff) + kp.grid_n[1] * (c >> 16));
+        };
+        auto load = [&](int l, int& a, int& b, float4* it) {
+            const uint4* r = reinterpret_cast<const uint4*>(kp.grid_cells + l);
+            const uint4 h = r[0];
+            it[0] = __builtin_bit_cast(float4, r[1]);
+            it[1] = __builtin_bit_cast(float4, r[2]);
+            it[2] = __builtin_bit_cast(float4, r[3]);
+            a = (int)h.x;
+            b = (int)h.y;
+        };
+        int lin = lin_of(cell);
+        int s0, s1;
+        float4 it[3];
+        load(lin, s0, s1, it);
+        for (;;) {
+            const int ix = cell & 0xff, iy = (cell >> 8) & 0xff, iz = cell >> 16;
+            int ncell;
+            vec3 ntm = tmx;
+            bool nvalid;
+            if (tmx.x <= tmx.y && tmx.x <= tmx.z) {
+                const int nx = d.x > 0.0f ? ix + 1 : ix - 1;
+                nvalid = !(nx < 0 || nx >= kp.grid_n[0]);
+                ncell = (cell & ~0xff) | (nx & 0xff);
+                ntm.x = ((kp.grid_g0[0] + (float)(d.x > 0.0f ? nx + 1 : nx) * kp.grid_h[0]) - o.x) * inv.x;
+            } else if (tmx.y <= tmx.z) {
+                const int ny = d.y > 0.0f ? iy + 1 : iy - 1;
+                nvalid = !(ny < 0 || ny >= kp.grid_n[1]);
+                ncell = (cell & ~0xff00) | (ny & 0xff) << 8;
+                ntm.y = ((kp.grid_g0[1] + (float)(d.y > 0.0f ? ny + 1 : ny) * kp.grid_h[1]) - o.y) * inv.y;
+            } else {
+                const int nz = d.z > 0.0f ? iz + 1 : iz - 1;
+                nvalid = !(nz < 0 || nz >= kp.grid_n[2]);
+                ncell = (cell & 0xffff) | (nz & 0xff) << 16;
+                ntm.z = ((kp.grid_g0[2] + (float)(d.z > 0.0f ? nz + 1 : nz) * kp.grid_h[2]) - o.z) * inv.z;
+            }
+            // the next record, unconditionally (this cell's again when there is none)
+            const int nlin = nvalid ? lin_of(ncell) : lin;
+            int n0, n1;
+            float4 nit[3];
+            load(nlin, n0, n1, nit);
+            if (COUNT) {
+                ++c_nodes;
+                c_tests += (uint32_t)(s1 - s0);
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (s0 + q < s1) accept(sphere_t(it[q].w, o - v3(it[q].x, it[q].y, it[q].z), d), s0 + q);
+            // items beyond the record (IPT_GRID_ITEMS loads in flight)
+            constexpr int X = IPT_GRID_ITEMS;
+            for (int k2 = s0 + 3; k2 < s1; k2 += X) {
+                float4 c4[X];
+#pragma unroll
+                for (int q = 0; q < X; ++q)
+                    c4[q] = *reinterpret_cast<const float4*>(kp.grid_items[k2 + q < s1 ? k2 + q : k2].c);
+#pragma unroll
+                for (int q = 0; q < X; ++q)
+                    if (k2 + q < s1) accept(sphere_t(c4[q].w, o - v3(c4[q].x, c4[q].y, c4[q].z), d), k2 + q);
+            }
+            --budget;
+            const float texit = fminf(fminf(tmx.x, tmx.y), tmx.z);
+            if (texit > (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f || !nvalid) {
+                cell = -1;
+                return;
+            }
+            cell = ncell;
+            tmx = ntm;
+            if (budget <= 0) return;
+            lin = nlin;
+            s0 = n0;
+            s1 = n1;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) it[q] = nit[q];
+        }
+    } else if constexpr (POS) {
         // the next cell (it depends on tmx alone) and its item range are
         // fetched before the current cell's items are tested, so the range
         // load overlaps the item loads; the exit test (on best) then decides
@@ -338,16 +430,16 @@ __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3
                 }
             };
             constexpr int X = IPT_GRID_ITEMS;
-            for (int k2 = s0; k2 < s1; k2 += X) {
-                float4 c4[X];
+                for (int k2 = s0; k2 < s1; k2 += X) {
+                    float4 c4[X];
 #pragma unroll
-                for (int q = 0; q < X; ++q)
-                    c4[q] = *reinterpret_cast<const float4*>(kp.grid_items[k2 + q < s1 ? k2 + q : k2].c);
-                test(c4[0], k2);
+                    for (int q = 0; q < X; ++q)
+                        c4[q] = *reinterpret_cast<const float4*>(kp.grid_items[k2 + q < s1 ? k2 + q : k2].c);
+                    test(c4[0], k2);
 #pragma unroll
-                for (int q = 1; q < X; ++q)
-                    if (k2 + q < s1) test(c4[q], k2 + q);
-            }
+                    for (int q = 1; q < X; ++q)
+                        if (k2 + q < s1) test(c4[q], k2 + q);
+                }
             --budget;
             const float texit = fminf(fminf(tmx.x, tmx.y), tmx.z);
             if (texit > (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f || !nvalid) {
@@ -1958,6 +2050,7 @@ struct ipt_ctx {
     int n_grid = 0;
     int* d_grid_start = nullptr;
     BvhSphere* d_grid_items = nullptr;
+    GridCell* d_grid_cells = nullptr;  // 64-byte cell records (IPT_GRID_INLINE)
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
@@ -2301,6 +2394,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.grid_m = ctx->grid.m;
         kp.grid_start = ctx->d_grid_start;
         kp.grid_items = ctx->d_grid_items;
+        kp.grid_cells = ctx->d_grid_cells;
         kp.bvh_prims = ctx->d_bvh_prims;
         kp.n_nodes = ctx->n_nodes;
         kp.light_nodes = ctx->d_light_nodes;
@@ -2443,7 +2537,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
-                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_frame_sc};
+                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_frame_sc};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& e : ctx->ev)
@@ -2587,6 +2681,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     };
     DevBuf<int> n_grid_start, n_lgrid, n_cdf_lo;
     DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
+    DevBuf<GridCell> n_grid_cells;
     DevBuf<BvhNode> n_light_nodes, n_bvh_nodes;
     DevBuf<LightDev> n_lights;
     DevBuf<float> n_weights, n_cdf;
@@ -2595,6 +2690,9 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     int rc = IPT_OK;
     if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
     if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
+    std::vector<GridCell> gcells;
+    if (use_grid) grid_cells_build(grid, gcells);
+    if (use_grid && !rc) rc = upload(n_grid_cells, gcells.data(), gcells.size());
     if (!lnodes.empty() && !rc) rc = upload(n_light_nodes, lnodes.data(), lnodes.size());
     if (lg.pattern && !rc) rc = upload(n_lgrid, lg.cells.data(), lg.cells.size());
     if (use_cdf_lo && !rc) rc = upload(n_cdf_lo, cdf_lo.data(), cdf_lo.size());
@@ -2607,12 +2705,13 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!rc) rc = upload(n_spheres, sph.data(), sph.size());
     if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
-                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_wall, ctx->d_lgrid,
+                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_wall, ctx->d_lgrid,
                    ctx->d_cdf_lo};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_grid_start = n_grid_start.release();
     ctx->d_grid_items = n_grid_items.release();
+    ctx->d_grid_cells = n_grid_cells.release();
     ctx->n_grid = 0;
     if (use_grid) {
         ctx->n_grid = (int)(grid.start.size() - 1);

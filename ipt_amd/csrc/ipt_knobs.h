@@ -8,7 +8,7 @@
 
 #if !defined(IPT_AB_BUILD) &&                                                                           \
     (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
-     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
+     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || \
@@ -72,6 +72,9 @@
 #endif
 
 // ---- walk budgets and acceleration-structure parameters
+#ifndef IPT_GRID_INLINE
+#define IPT_GRID_INLINE 1  // pipelined grid walk over 64-byte cell records (range + first 3 items inline)
+#endif
 #ifndef IPT_GRID_BUDGET
 #define IPT_GRID_BUDGET 5  // grid cells per lane per step of a resumable walk (measured 4-32)
 #endif

@@ -251,8 +251,6 @@ Scene make_scene_by_name(const std::string& spec) {
     if (n == "square_lit_by_square" || n == "floor") return make_scene_square_lit_by_square();
     if (n == "lit_corner" || n == "corner") return make_scene_lit_corner();
     if (n == "smallpt") return make_scene_smallpt();
-    if (n == "square_lit_by_square") return make_scene_square_lit_by_square();
-    if (n == "lit_corner") return make_scene_lit_corner();
     throw IptError(IPT_E_INVALID, "unknown scene '" + spec + "'");
 }
 

@@ -60,3 +60,26 @@ done
 if [ "${IPT_REGEN_GOLDEN:-0}" = "1" ] || [ ! -f "$GOLDEN/ref_rotate.bin" ]; then
   "$OUT/ref_kat" "$GOLDEN"
 fi
+
+# INTEGRATION.md §1's reference-side adapter (integration/render_gpu.cpp),
+# type-checked and linked against the reference's own headers and TUs. The
+# one change the adapter documents -- public accessors for AreaLight's private
+# x_axis / y_axis / type (lighting.h:20-23) -- is applied to a temporary copy
+# of lighting.h outside the repository (removed below; nothing of it is kept).
+# Output: oracle/_ref/adapter_check (runs the adapter on the reference's
+# make_scene_box(), tests/test_reference_adapter.py).
+LIB_DIR="$HERE/../ipt_amd/lib"
+if [ -f "$LIB_DIR/libipt_hip.so" ]; then
+  PATCH=$(mktemp -d)
+  mkdir -p "$PATCH/lighting"
+  sed 's|^\(    AreaLight(glm::vec3 origin.*\)$|    glm::vec3 xAxis() const { return x_axis; }\n    glm::vec3 yAxis() const { return y_axis; }\n    type_t lightType() const { return type; }\n\1|' \
+    "$REF/src/lighting/lighting.h" > "$PATCH/lighting/lighting.h"
+  grep -q "lightType()" "$PATCH/lighting/lighting.h" || { echo "build_ref: accessor patch did not apply"; rm -rf "$PATCH"; exit 1; }
+  rc=0
+  "$CXX" -std=c++17 -O2 -DBOOST_POOLFWD_HPP -I"$PATCH" "${FLAGS[@]:3}" -I"$HERE/../include" \
+    "$HERE/../integration/render_gpu.cpp" "$HERE/../integration/adapter_check.cpp" "${objs[@]}" \
+    -L"$LIB_DIR" -lipt_hip -Wl,-rpath,'$ORIGIN/../../ipt_amd/lib' -Wl,-rpath-link,/opt/rocm/lib \
+    -Wl,--unresolved-symbols=ignore-in-object-files -o "$OUT/adapter_check" || rc=$?
+  rm -rf "$PATCH"
+  [ $rc -eq 0 ] || exit $rc
+fi
