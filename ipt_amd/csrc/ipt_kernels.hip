@@ -75,6 +75,7 @@ struct KParams {
     float bvh_tmargin;                    // sphere BVH / grid: additive pruning margin (1e-3 D, ipt_bvh.h)
     int n_grid;                           // > 0: uniform sphere grid (ipt_bvh.h SphereGrid) instead of the BVH
     float grid_g0[3], grid_h[3], grid_inv_h[3], grid_m;
+    float grid_g1[3];                     // g0 + (float)n * h, the grid's far corner (host-computed)
     int grid_n[3];
     const int* __restrict__ grid_start;   // [cells + 1]
     const GridCell* __restrict__ grid_cells;  // [cells] range + first three items (IPT_GRID_INLINE)
@@ -253,7 +254,7 @@ __device__ __forceinline__ void sphere_grid_init(const KParams& kp, vec3 o, vec3
     const float dv[3] = {d.x, d.y, d.z}, ov[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
     float tn = 0.0f, tf = inf_();
     for (int a = 0; a < 3; ++a) {
-        const float g1 = kp.grid_g0[a] + (float)kp.grid_n[a] * kp.grid_h[a];
+        const float g1 = kp.grid_g1[a];  // g0 + (float)n * h
         if (dv[a] == 0.0f) {
             if (ov[a] < kp.grid_g0[a] || ov[a] > g1) tf = -1.0f;  // parallel and outside
             continue;
@@ -675,7 +676,7 @@ __host__ __device__ constexpr bool resumable_lights(int lmode, int geom) {
     return IPT_RESUME_LIGHTS && lmode == 3 /* kLightsGlobal */ && !resumable_geom(geom);
 }
 __host__ __device__ constexpr int waves_per_simd(int geom, int lmode) {
-    return (resumable_geom(geom) || resumable_lights(lmode, geom)) ? IPT_RES_WAVES : IPT_WAVES_PER_SIMD;
+    return resumable_geom(geom) ? IPT_RES_WAVES : (resumable_lights(lmode, geom) ? IPT_RESL_WAVES : IPT_WAVES_PER_SIMD);
 }
 // render_sample's per-sample work before ray_power (main.cpp:192-211) for
 // work unit `unit` (pass-major, then candidate row, then column): the absolute
@@ -807,8 +808,10 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     if (one_light(LMODE)) {
         LS.one = kp.lights[0];
         // held in VGPRs (+3.5 % C2; area and spow stay uniform)
-        vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y);
-        vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]);
+        if (IPT_RES_HOLD || !resumable_geom(GEOM)) {
+            vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y);
+            vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]);
+        }
         LS.w0 = kp.weights[0];
         LS.c0 = kp.cdf[0];
         LS.c1 = kp.cdf[1];
@@ -838,7 +841,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
 
     // the sphere grid walk's parameters (kRes instances), held in VGPRs (+5 % C3)
     KParams kg = kp;
-    if (resumable_geom(GEOM)) {
+    if (IPT_RES_HOLD && resumable_geom(GEOM)) {
         for (int a = 0; a < 3; ++a) {
             vgpr_hold(kg.grid_g0[a]);
             vgpr_hold(kg.grid_h[a]);
@@ -1031,6 +1034,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
         // for a cosine pick, the CosineDdf table gathers (running it one step
         // ahead, right after the direction phase, measured -2.7 %: DESIGN.md 4.3)
         const bool iter_lane = active && has_path && !fresh && !((kRes || kResL) && tracing);
+        if constexpr (kRes) {
+            // the iteration's pick, draws and CosineDdf factors live within the
+            // step (set by the prologue / gathers, used by the direction phase):
+            // overwritten here, they are not carried across the step loop's back
+            // edge (-13 VGPRs: the sphere-list instances fit 4 waves per SIMD;
+            // the others measured 1 % slower this way)
+            pick = -1;
+            u1 = u2 = tr = cs_c = cs_s = 0.0f;
+        }
         // the cosine pick's table indices; the gathers are issued by the whole
         // wave after the prologue (index 0 for the other lanes) so that the
         // number of loads between a gather and its wait is the same on every
@@ -2390,6 +2402,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
             kp.grid_h[a] = ctx->grid.h[a];
             kp.grid_inv_h[a] = ctx->grid.inv_h[a];
             kp.grid_n[a] = ctx->grid.n[a];
+            kp.grid_g1[a] = ctx->grid.g0[a] + (float)ctx->grid.n[a] * ctx->grid.h[a];
         }
         kp.grid_m = ctx->grid.m;
         kp.grid_start = ctx->d_grid_start;
@@ -2691,8 +2704,8 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
     if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
     std::vector<GridCell> gcells;
-    if (use_grid) grid_cells_build(grid, gcells);
-    if (use_grid && !rc) rc = upload(n_grid_cells, gcells.data(), gcells.size());
+    if (IPT_GRID_INLINE && use_grid) grid_cells_build(grid, gcells);
+    if (IPT_GRID_INLINE && use_grid && !rc) rc = upload(n_grid_cells, gcells.data(), gcells.size());
     if (!lnodes.empty() && !rc) rc = upload(n_light_nodes, lnodes.data(), lnodes.size());
     if (lg.pattern && !rc) rc = upload(n_lgrid, lg.cells.data(), lg.cells.size());
     if (use_cdf_lo && !rc) rc = upload(n_cdf_lo, cdf_lo.data(), cdf_lo.size());

@@ -10,7 +10,7 @@
     (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
      defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
-     defined(IPT_RES_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
+     defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE))
@@ -25,7 +25,14 @@
 #define IPT_WAVES_PER_SIMD 4  // __launch_bounds__ occupancy of the non-resumable instances
 #endif
 #ifndef IPT_RES_WAVES
-#define IPT_RES_WAVES 3  // ... of the resumable (sphere-list, many-light BVH) instances
+#define IPT_RES_WAVES 4  // ... of the resumable sphere-list instances (C3: 3 -> 4 waves +12 %)
+#endif
+#ifndef IPT_RESL_WAVES
+#define IPT_RESL_WAVES 3  // ... of the resumable many-light (light BVH) instances
+#endif
+#ifndef IPT_RES_HOLD
+#define IPT_RES_HOLD 0  // sphere-list instances hold the single light and the grid parameters in
+                        // VGPRs (+5 % at 3 waves; at 4 waves the registers are needed, -30 %)
 #endif
 
 // ---- structure (each also has a runtime or scene condition)
@@ -73,7 +80,7 @@
 
 // ---- walk budgets and acceleration-structure parameters
 #ifndef IPT_GRID_INLINE
-#define IPT_GRID_INLINE 1  // pipelined grid walk over 64-byte cell records (range + first 3 items inline)
+#define IPT_GRID_INLINE 0  // 1: the grid walk over 64-byte cell records (range + first 3 items inline): C3 -9 %
 #endif
 #ifndef IPT_GRID_BUDGET
 #define IPT_GRID_BUDGET 5  // grid cells per lane per step of a resumable walk (measured 4-32)
