@@ -88,6 +88,7 @@ struct KParams {
     int lnodes_lds;                       // light BVH staged in LDS (kLightsGlobal)
     // kLightsGridA10/A01: coplanar axis-aligned lights on a lattice (LightGrid)
     const int* __restrict__ lgrid;        // [lg_nu * lg_nv] light index per cell, -1 = none
+    const float4* __restrict__ lax;       // [n_lights][3] LightAx records (IPT_LIGHT_AX_REC)
     int lg_nu, lg_nv;
     float lg_u0, lg_v0, lg_icw, lg_ich;   // cell coordinates: (q - u0) * icw
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
@@ -1068,7 +1069,16 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                     cs_s = sp;
                 }
             } else {
-                if constexpr (grid_lights(LMODE) && IPT_LPF) {
+                if constexpr (grid_lights(LMODE) && IPT_LPF && IPT_LIGHT_AX_REC) {
+                    // the compact record's first 16 bytes: P.xy, x[XA], y[YA]
+                    // (P.z, n.z: the lattice plane; lattice lights are diamonds)
+                    const float4 a = kp.lax[3 * ((ran && pick >= 0 && pick < nl) ? pick : 0)];
+                    lpP = v3(a.x, a.y, kp.lg_pn);
+                    lpx = a.z;
+                    lpy = a.w;
+                    lpn = kp.lg_nn;
+                    lptype = 0;
+                } else if constexpr (grid_lights(LMODE) && IPT_LPF) {
                     constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
                     const LightDev& Ls = kp.lights[(ran && pick >= 0 && pick < nl) ? pick : 0];
                     lpP = Ls.P;
@@ -1505,16 +1515,39 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             bool has_li = false;
             vec3 li_pos = v3(0, 0, 0);
             float li_pow = 0.0f;
-            auto light_step = [&](int l) {
-                const LightDev& L = LS.light(l);
+            auto light_step_with = [&](const LightDev& L, float wl) {
                 vec3 hp, hn;
                 const bool h = ltrace(L, ro, rd, &hp, &hn);
                 if (COUNT) ++c_ltest;
-                if (is_iter) lmix += LS.weight(l) * lpdf(L, ro, h, hp, hn);
+                if (is_iter) lmix += wl * lpdf(L, ro, h, hp, hn);
                 if (h && (!has_li || longer(li_pos - ro, hp - ro))) {
                     has_li = true;
                     li_pos = hp;
                     li_pow = L.spow;
+                }
+            };
+            auto light_step = [&](int l) {
+                if constexpr (grid_lights(LMODE) && IPT_LIGHT_AX_REC) {
+                    // the lattice light from its 48-byte record: exactly the
+                    // fields light_trace_ax / light_pdf_ax read (ipt_path.h LightAx)
+                    constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                    const float4* r = kp.lax + 3 * l;
+                    const float4 a = r[0], b = r[1], c = r[2];
+                    LightDev L;
+                    L.P = v3(a.x, a.y, kp.lg_pn);
+                    L.x = XA == 0 ? v3(a.z, 0.0f, 0.0f) : v3(0.0f, a.z, 0.0f);
+                    L.y = YA == 0 ? v3(a.w, 0.0f, 0.0f) : v3(0.0f, a.w, 0.0f);
+                    L.n = v3(0.0f, 0.0f, kp.lg_nn);
+                    L.inv.c[XA] = v3(b.x, 0.0f, 0.0f);
+                    L.inv.c[YA] = v3(0.0f, b.y, 0.0f);
+                    L.inv.c[2] = v3(0.0f, 0.0f, 0.0f);
+                    L.area = b.z;
+                    L.spow = b.w;
+                    L.type = 0;
+                    L.pad = 0;
+                    light_step_with(L, c.x);
+                } else {
+                    light_step_with(LS.light(l), LS.weight(l));
                 }
             };
             // the reference's event count: every light traced once for the
@@ -2071,6 +2104,7 @@ struct ipt_ctx {
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
     LightGrid lgrid;     // lgrid.pattern != 0: coplanar light lattice (kLightsGridA10/A01)
     int* d_lgrid = nullptr;
+    LightAx* d_lax = nullptr;  // lattice lights' compact records (IPT_LIGHT_AX_REC)
     int bpc_override = 0;
     int lnodes_lds = 1;  // stage the light BVH in LDS (IPT_LNODES_LDS=0: global memory)
     int light_grid_on = 1;  // coplanar light lattices by cell lookup (IPT_LIGHT_GRID=0: the light BVH)
@@ -2419,6 +2453,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cdf_bsearch = ctx->cdf_bsearch;
         kp.cdf_lo = ctx->d_cdf_lo;
         kp.lgrid = ctx->d_lgrid;
+        kp.lax = reinterpret_cast<const float4*>(ctx->d_lax);
         kp.lg_nu = ctx->lgrid.nu;
         kp.lg_nv = ctx->lgrid.nv;
         kp.lg_u0 = ctx->lgrid.u0;
@@ -2547,7 +2582,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
 void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
-    void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
+    void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_lax, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
                     ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_frame_sc};
@@ -2693,6 +2728,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         return IPT_OK;
     };
     DevBuf<int> n_grid_start, n_lgrid, n_cdf_lo;
+    DevBuf<LightAx> n_lax;
     DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
     DevBuf<GridCell> n_grid_cells;
     DevBuf<BvhNode> n_light_nodes, n_bvh_nodes;
@@ -2708,6 +2744,10 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (IPT_GRID_INLINE && use_grid && !rc) rc = upload(n_grid_cells, gcells.data(), gcells.size());
     if (!lnodes.empty() && !rc) rc = upload(n_light_nodes, lnodes.data(), lnodes.size());
     if (lg.pattern && !rc) rc = upload(n_lgrid, lg.cells.data(), lg.cells.size());
+    std::vector<LightAx> laxr;
+    if (lg.pattern)
+        for (int i = 0; i < nl; ++i) laxr.push_back(light_ax_record(L[i], lg.pattern, wts[i]));
+    if (lg.pattern && !rc) rc = upload(n_lax, laxr.data(), laxr.size());
     if (use_cdf_lo && !rc) rc = upload(n_cdf_lo, cdf_lo.data(), cdf_lo.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_nodes, bnodes.data(), bnodes.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_prims, bprims.data(), bprims.size());
@@ -2718,7 +2758,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!rc) rc = upload(n_spheres, sph.data(), sph.size());
     if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
-                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_wall, ctx->d_lgrid,
+                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_wall, ctx->d_lgrid, ctx->d_lax,
                    ctx->d_cdf_lo};
     for (void* b : old)
         if (b) hipFree(b);
@@ -2736,6 +2776,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->d_light_nodes = n_light_nodes.release();
     ctx->n_light_nodes = lnodes.empty() ? 0 : n_lnodes;
     ctx->d_lgrid = n_lgrid.release();
+    ctx->d_lax = n_lax.release();
     ctx->d_cdf_lo = n_cdf_lo.release();
     lg.cells.clear();
     ctx->lgrid = lg;
