@@ -93,7 +93,7 @@ EXPORTED_SYMBOLS = (
 
 # path-kernel phases of the IPT_PROF profile (ipt_kernels.hip IPT_PHASE ids)
 PROFILE_PHASES = ("step", "pop", "new_path", "iteration", "philox", "frame_worker",
-                  "cosine_worker", "light_sample", "trace", "geometry", "push", "wg_step")
+                  "walk_cell", "light_sample", "trace", "geometry", "push", "wg_step")
 # step segments of the IPT_STAMP diagnostic build (IPT_STAMP_AT ids)
 STAMP_SEGMENTS = ("loop_top", "refill", "pop_early", "pre_prologue", "prologue_philox_frame", "exit_test",
                   "pop", "frame_prefetch", "new_path_direction", "lights", "mixture_geometry", "resolve_push")

@@ -61,6 +61,18 @@ constexpr int kStamps = 12;
         __builtin_amdgcn_sched_barrier(0);                                         \
     }
 
+// IPT_PROF: device functions with their own hooks take the arrays as extra
+// parameters (nothing in other builds)
+#if IPT_PROF
+#define IPT_DIAG_PARAMS , uint32_t *prof_w, uint32_t *prof_l
+#define IPT_DIAG_ARGS , prof_w, prof_l
+#define IPT_DIAG_NULL_ARGS , nullptr, nullptr
+#else
+#define IPT_DIAG_NULL_ARGS
+#define IPT_DIAG_PARAMS
+#define IPT_DIAG_ARGS
+#endif
+
 // the hooks' per-lane state, declared at the top of the kernel
 #define IPT_DIAG_STATE                                                                    \
     uint32_t prof_w[kProfPhases], prof_l[kProfPhases];                                    \

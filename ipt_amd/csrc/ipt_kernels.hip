@@ -289,7 +289,8 @@ __device__ __forceinline__ void sphere_grid_init(const KParams& kp, vec3 o, vec3
 // their tests, and the next cell's item range is fetched with them.
 template <bool COUNT, bool POS = false>
 __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3 d, int& cell, vec3& tmx, float& best,
-                                                 int& bidx, int budget, uint32_t& c_nodes, uint32_t& c_tests) {
+                                                 int& bidx, int budget, uint32_t& c_nodes,
+                                                 uint32_t& c_tests IPT_DIAG_PARAMS) {
     const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     auto accept = [&](float t, int k2) {  // FractalSpheres.cpp:75-84's rule on item positions
         if (isfinite_(t) && gt_1em6(fabs_(t))) {
@@ -394,6 +395,9 @@ __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3
         int lin = lin_of(cell);
         int s0 = kp.grid_start[lin], s1 = kp.grid_start[lin + 1];
         for (;;) {
+#if IPT_PROF
+            if (prof_w) { IPT_PHASE(6); }  // one cell of the pipelined walk
+#endif
             const int ix = cell & 0xff, iy = (cell >> 8) & 0xff, iz = cell >> 16;
             int ncell;
             vec3 ntm = tmx;
@@ -560,7 +564,7 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
         int cell;
         vec3 tmx;
         sphere_grid_init(kp, o, d, cell, tmx);
-        sphere_grid_walk<COUNT>(kp, o, d, cell, tmx, best, bidx, 0x7fffffff, c_nodes, c_tests);
+        sphere_grid_walk<COUNT>(kp, o, d, cell, tmx, best, bidx, 0x7fffffff, c_nodes, c_tests IPT_DIAG_NULL_ARGS);
     } else if (kp.n_nodes > 0) {
         int i = 0;
         sphere_bvh_walk<COUNT>(kp, o, d, i, best, bidx, 0x7fffffff, c_nodes, c_tests);
@@ -1667,7 +1671,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             bool done;
             if (kp.n_grid > 0) {
                 sphere_grid_walk<COUNT, IPT_GRID_PIPE != 0>(kg, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET, c_nodes,
-                                                          c_tests);
+                                                          c_tests IPT_DIAG_ARGS);
                 done = xi < 0;
             } else {
                 sphere_bvh_walk<COUNT>(kp, xro, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
