@@ -6,6 +6,7 @@
 #   src/geometry/geometric_utils.cpp                 (needs nothing but glm)
 #   src/SimpleCamera.cpp src/GridRenderPlane.cpp src/CollectionLighting.cpp
 #   src/lighting/lighting.cpp src/sample_scenes.cpp src/geometry/*.cpp
+#   src/gui.cpp (only its static glare(), through oracle/ref_glare.cpp)
 # These include libddf/ddf.h, which includes <boost/pool/poolfwd.hpp>; that
 # header needs <boost/config.hpp>, which this image does not have. None of
 # these TUs uses anything poolfwd.hpp declares, so its include guard is
@@ -59,6 +60,17 @@ done
 # regenerate the committed fixtures only when asked (they are checked in)
 if [ "${IPT_REGEN_GOLDEN:-0}" = "1" ] || [ ! -f "$GOLDEN/ref_rotate.bin" ]; then
   "$OUT/ref_kat" "$GOLDEN"
+fi
+
+# Gui's glare (gui.cpp:38-52) is a static function of the gui.cpp TU; the
+# harness oracle/ref_glare.cpp includes that TU where it lies (CImg.h is
+# header-only under $REF/include; X11 is linked but no display is opened) and
+# writes tests/golden/ref_glare.bin.
+if [ ! -f "$OUT/ref_glare" ] || [ "$HERE/ref_glare.cpp" -nt "$OUT/ref_glare" ]; then
+  "$CXX" "${FLAGS[@]}" "$HERE/ref_glare.cpp" "$OUT/SimpleCamera.o" -o "$OUT/ref_glare" -lX11 -lpthread
+fi
+if [ "${IPT_REGEN_GOLDEN:-0}" = "1" ] || [ ! -f "$GOLDEN/ref_glare.bin" ]; then
+  "$OUT/ref_glare" "$GOLDEN"
 fi
 
 # INTEGRATION.md §1's reference-side adapter (integration/render_gpu.cpp),

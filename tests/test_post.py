@@ -1,8 +1,10 @@
 """Image post-process: GridRenderPlane::smooth /
 computeSmoothedMax and Gui's glare, on the GPU (ipt_amd/csrc/ipt_post.hip),
 bit-exact. CPU: the oracle restatement against the reference's own compiled
-GridRenderPlane (tests/golden/ref_smooth.bin from oracle/ref_kat.cpp) and the
-hypot identity the glare kernel uses. GPU: kernels against the oracle."""
+GridRenderPlane (tests/golden/ref_smooth.bin from oracle/ref_kat.cpp), against
+the reference's own gui.cpp glare() (tests/golden/ref_glare.bin from
+oracle/ref_glare.cpp) and the hypot identity the glare kernel uses. GPU:
+kernels against both golden files and the oracle."""
 import ctypes as C
 import subprocess
 from pathlib import Path
@@ -15,6 +17,7 @@ from ipt_amd import capi
 
 HERE = Path(__file__).resolve().parent
 GOLD = HERE / "golden" / "ref_smooth.bin"
+GOLD_GLARE = HERE / "golden" / "ref_glare.bin"  # reference gui.cpp glare(), oracle/ref_glare.cpp
 
 
 def _lib():
@@ -55,6 +58,30 @@ def _cases():
         out.append((W, H, side, inp, sm, d[pos], d[pos + 1]))
         pos += 2
     return out
+
+
+def _glare_cases():
+    d = np.fromfile(GOLD_GLARE, np.float32)
+    n, pos, out = int(d[0]), 1, []
+    for _ in range(n):
+        W, H, cutoff = int(d[pos]), int(d[pos + 1]), d[pos + 2]
+        pos += 3
+        inp = d[pos:pos + W * H]; pos += W * H
+        ref = d[pos:pos + W * H]; pos += W * H
+        out.append((W, H, cutoff, inp, ref))
+    return out
+
+
+def test_oracle_glare_matches_reference(oracle):
+    """The oracle's glare against the reference's own gui.cpp glare() (9 cases:
+    single hot pixel at the GUI cutoff 1.01, random hot fractions, a pixel at /
+    just above the cutoff, negative pixels, +inf and NaN sources, 1x1, 1xN)."""
+    cases = _glare_cases()
+    assert len(cases) == 9
+    assert any(np.isnan(r).all() for *_, r in cases)
+    for W, H, cutoff, inp, ref in cases:
+        got = oracle_glare(inp, W, H, float(cutoff))
+        assert np.array_equal(_bits(got), _bits(ref)), (W, H, float(cutoff))
 
 
 def test_oracle_smooth_matches_reference(oracle):
@@ -104,6 +131,13 @@ def test_gpu_smooth_matches_reference_and_oracle(gpu_ctx, oracle):
         assert np.array_equal(_bits(got), _bits(ref)) and _bits(mx) == _bits(rmx), (W, H, side)
     with pytest.raises(capi.IptError):
         gpu_ctx.smooth(px, W, H, 1, True)
+
+
+@pytest.mark.gpu
+def test_gpu_glare_matches_reference(gpu_ctx):
+    for W, H, cutoff, inp, ref in _glare_cases():
+        got = gpu_ctx.glare(inp, W, H, float(cutoff))
+        assert np.array_equal(_bits(got), _bits(ref)), (W, H, float(cutoff))
 
 
 @pytest.mark.gpu
