@@ -94,7 +94,6 @@ struct KParams {
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
-    int cand_lds;                         // candidate rows staged in LDS (sharded, n_cand <= kLdsCand)
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
     int box_inrange;                      // camera and sphere list within 2^39 (box_plane_t<true>)
@@ -589,7 +588,6 @@ __device__ __forceinline__ float trace_geometry(const KParams& kp, vec3 o, vec3 
 // the candidate-row table live in LDS after the DFS stack.
 constexpr int kLdsLights = 16;
 constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
-constexpr int kLdsCand = 512;
 // LDS after the DFS stack: frames, [LMODE 2: lights, weights, cdf],
 // [sharded: candidate rows], [LMODE 3: weights, cdf, light BVH].
 // Frames live in LDS, [12][kFrameStride]: column tid is the lane's current
@@ -599,8 +597,16 @@ constexpr int kLdsCand = 512;
 // 64 dwords, so a column's 12 words pair into ds_read2st64/ds_write2st64;
 // 2.7 KiB more, still 4 workgroups/CU); the others keep kBlock + 8 so that
 // their light data fits 4 workgroups as well.
+// Threads per workgroup of a path-kernel instance: kBlock, or one 1024-thread
+// workgroup per CU for the light lattices with their records in LDS
+// (kLightsGridA10L/A01L: the per-lane LDS is the same, the shared tables and
+// records are held once per CU instead of once per 256-thread workgroup).
+constexpr int kLatticeBlock = 1024;
+__host__ __device__ constexpr int block_of(int lmode) {
+    return (lmode == 9 || lmode == 10) ? kLatticeBlock : kBlock;
+}
 __host__ __device__ constexpr int frame_stride(int lmode) {
-    return (lmode == 1 || lmode == 5 || lmode == 6) ? kBlock + 64 : kBlock + 8;
+    return (lmode == 1 || lmode == 5 || lmode == 6) ? block_of(lmode) + 64 : block_of(lmode) + 8;
 }
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
     return 12 * (size_t)frame_stride(lmode) +
@@ -627,12 +633,16 @@ __host__ __device__ inline size_t global_light_lds_words(int nl, int n_nodes_lds
 // generic/flat pointer is ever formed: a flat load would make the compiler
 // wait for every outstanding radiance store).
 enum { kLightsOne = 1, kLightsLds = 2, kLightsGlobal = 3, kLightsAny = 4, kLightsOneA10 = 5, kLightsOneA01 = 6,
-       kLightsGridA10 = 7, kLightsGridA01 = 8 };
+       kLightsGridA10 = 7, kLightsGridA01 = 8, kLightsGridA10L = 9, kLightsGridA01L = 10 };
 // kLightsGridA10 / A01: many AreaLights, all axis-aligned with the same axis
 // pattern, sharing their plane and lying on a lattice, one per cell
 // (light_grid_build): a ray's lights are found by its plane point's cell(s)
 // instead of the light BVH walk; weights and CDF staged as kLightsGlobal.
-__host__ __device__ constexpr bool grid_lights(int lm) { return lm == kLightsGridA10 || lm == kLightsGridA01; }
+// kLightsGridA10L / A01L: the same with the 48-byte records in LDS, one
+// 1024-thread workgroup per CU (block_of), chosen when the LDS fits (+5 % C5)
+__host__ __device__ constexpr bool grid_lights(int lm) { return lm >= kLightsGridA10 && lm <= kLightsGridA01L; }
+__host__ __device__ constexpr bool lattice_a10(int lm) { return lm == kLightsGridA10 || lm == kLightsGridA10L; }
+__host__ __device__ constexpr bool lax_in_lds(int lm) { return lm == kLightsGridA10L || lm == kLightsGridA01L; }
 __host__ __device__ constexpr bool global_lights(int lm) { return lm == kLightsGlobal || grid_lights(lm); }
 // kLightsOneA10 / A01: the single light is an axis-aligned AreaLight
 // (axis_aligned_light, ipt_path.h) with x_axis along y and y_axis along x
@@ -754,7 +764,8 @@ __global__ __launch_bounds__(256) void raygen_kernel(const KParams kp) {
 }
 
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
-__global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
+__global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
+    constexpr int kBlock = block_of(LMODE);  // this instance's workgroup size
     extern __shared__ float lds[];
     float* stk = lds;                                         // [MAXSUSP][F][kBlock]
     constexpr int kFrameStride = frame_stride(LMODE);
@@ -762,19 +773,19 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride);
     float* weights_lds = reinterpret_cast<float*>(lights_lds) + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
-    int* cand_lds = reinterpret_cast<int*>(reinterpret_cast<float*>(lights_lds) +
-                                           (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0));
-                                           // [kLdsCand] when kp.cand_lds
-    // kLightsGlobal: [weights | cdf | light BVH nodes] after the candidate rows
-    float* gl_lds = reinterpret_cast<float*>(cand_lds) + (kp.cand_lds ? kLdsCand : 0);
+    // kLightsGlobal: [weights | cdf | light BVH nodes] after the frames
+    float* gl_lds = reinterpret_cast<float*>(lights_lds) +
+                    (LMODE == kLightsLds ? kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0);
     constexpr bool kGridL = grid_lights(LMODE);
     BvhNode* lnodes_lds = reinterpret_cast<BvhNode*>(gl_lds + global_light_prefix_words(kp.n_lights, kGridL));
     float* cdf_gl = gl_lds + (kGridL ? 0 : kp.n_lights + 1);
+    // kLightsGridA10L/A01L: the lattice lights' records after the cells (16-byte aligned)
+    constexpr bool kLaxLds = lax_in_lds(LMODE);
+    float4* lax_lds = reinterpret_cast<float4*>(reinterpret_cast<int*>(lnodes_lds) + ((kp.lg_nu * kp.lg_nv + 3) & ~3));
     int* cdf_lo_lds = reinterpret_cast<int*>(cdf_gl + kp.n_lights + 1);
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
-    const bool cand_in_lds = kp.cand_lds != 0;
     if (tid < 60) lfr[(tid % 12) * kFrameStride + kBlock + tid / 12] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
     if (LMODE == kLightsLds) {
         const float* src = reinterpret_cast<const float*>(kp.lights);
@@ -785,8 +796,6 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             cdf_lds[i] = kp.cdf[i];
         }
     }
-    if (cand_in_lds)
-        for (int i = tid; i < kp.n_cand; i += kBlock) cand_lds[i] = kp.cand_rows[i];
     if (global_lights(LMODE)) {
         for (int i = tid; i <= kp.n_lights; i += kBlock) {
             if (!kGridL) gl_lds[i] = kp.weights[i];
@@ -796,6 +805,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
             for (int i = tid; i < kCdfBuckets; i += kBlock) cdf_lo_lds[i] = kp.cdf_lo[i];
         if (grid_lights(LMODE))
             for (int i = tid; i < kp.lg_nu * kp.lg_nv; i += kBlock) reinterpret_cast<int*>(lnodes_lds)[i] = kp.lgrid[i];
+        if (kLaxLds)
+            for (int i = tid; i < 3 * kp.n_lights; i += kBlock) lax_lds[i] = kp.lax[i];
         if (LMODE == kLightsGlobal && kp.lnodes_lds) {
             const float4* src = reinterpret_cast<const float4*>(kp.light_nodes);
             float4* dst = reinterpret_cast<float4*>(lnodes_lds);
@@ -827,8 +838,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     auto ltrace = [&](const LightDev& L, vec3 o, vec3 d, vec3* hp, vec3* hn) -> bool {
         if constexpr (LMODE == kLightsOneA10) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
         else if constexpr (LMODE == kLightsOneA01) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
-        else if constexpr (LMODE == kLightsGridA10) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
-        else if constexpr (LMODE == kLightsGridA01) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
+        else if constexpr (grid_lights(LMODE) && lattice_a10(LMODE)) return light_trace_ax<1, 0, IPT_LIGHT_INR>(L, o, d, hp, hn);
+        else if constexpr (grid_lights(LMODE)) return light_trace_ax<0, 1, IPT_LIGHT_INR>(L, o, d, hp, hn);
         else return light_trace<LMODE == kLightsAny>(L, o, d, hp, hn);
     };
     auto lpdf = [&](const LightDev& L, vec3 o, bool h, vec3 hp, vec3 hn) -> float {
@@ -839,8 +850,8 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
     auto lsample = [&](const LightDev& L, vec3 o, float a, float b) -> vec3 {
         if constexpr (LMODE == kLightsOneA10) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
         else if constexpr (LMODE == kLightsOneA01) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
-        else if constexpr (LMODE == kLightsGridA10) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
-        else if constexpr (LMODE == kLightsGridA01) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
+        else if constexpr (grid_lights(LMODE) && lattice_a10(LMODE)) return light_sample_dir_ax<1, 0, IPT_LIGHT_INR>(L, o, a, b);
+        else if constexpr (grid_lights(LMODE)) return light_sample_dir_ax<0, 1, IPT_LIGHT_INR>(L, o, a, b);
         else return light_sample_dir<LMODE == kLightsAny>(L, o, a, b);
     };
 
@@ -1076,14 +1087,15 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if constexpr (grid_lights(LMODE) && IPT_LPF && IPT_LIGHT_AX_REC) {
                     // the compact record's first 16 bytes: P.xy, x[XA], y[YA]
                     // (P.z, n.z: the lattice plane; lattice lights are diamonds)
-                    const float4 a = kp.lax[3 * ((ran && pick >= 0 && pick < nl) ? pick : 0)];
+                    const int li = 3 * ((ran && pick >= 0 && pick < nl) ? pick : 0);
+                    const float4 a = kLaxLds ? lax_lds[li] : kp.lax[li];
                     lpP = v3(a.x, a.y, kp.lg_pn);
                     lpx = a.z;
                     lpy = a.w;
                     lpn = kp.lg_nn;
                     lptype = 0;
                 } else if constexpr (grid_lights(LMODE) && IPT_LPF) {
-                    constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                    constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
                     const LightDev& Ls = kp.lights[(ran && pick >= 0 && pick < nl) ? pick : 0];
                     lpP = Ls.P;
                     lpx = comp<XA>(Ls.x);
@@ -1320,7 +1332,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 IPT_PHASE(7);
                 if constexpr (grid_lights(LMODE) && IPT_LPF) {
                     // the gathered fields are all light_sample_dir_ax reads
-                    constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                    constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
                     dir = light_sample_dir_axf<XA, YA, IPT_LIGHT_INR>(lpP, lpx, lpy, lpn, lptype, tpos, u1, u2);
                 } else
                 dir = lsample(LS.light(pick), tpos, u1, u2);
@@ -1534,9 +1546,14 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 if constexpr (grid_lights(LMODE) && IPT_LIGHT_AX_REC) {
                     // the lattice light from its 48-byte record: exactly the
                     // fields light_trace_ax / light_pdf_ax read (ipt_path.h LightAx)
-                    constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
-                    const float4* r = kp.lax + 3 * l;
-                    const float4 a = r[0], b = r[1], c = r[2];
+                    constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
+                    float4 a, b, c;
+                    if constexpr (kLaxLds) {
+                        a = lax_lds[3 * l]; b = lax_lds[3 * l + 1]; c = lax_lds[3 * l + 2];
+                    } else {
+                        const float4* r = kp.lax + 3 * l;
+                        a = r[0]; b = r[1]; c = r[2];
+                    }
                     LightDev L;
                     L.P = v3(a.x, a.y, kp.lg_pn);
                     L.x = XA == 0 ? v3(a.z, 0.0f, 0.0f) : v3(0.0f, a.z, 0.0f);
@@ -1564,7 +1581,7 @@ __global__ __launch_bounds__(kBlock, waves_per_simd(GEOM, LMODE)) void path_kern
                 // the rounding of u, v are far below it), so the lights of those
                 // <= 4 cells, in index order, are the scan's hits (a light that
                 // is not hit adds +0 to lmix and is never nearest)
-                constexpr int XA = LMODE == kLightsGridA10 ? 1 : 0, YA = 1 - XA;
+                constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
                 const float n_dir = kp.lg_nn * comp<2>(rd);
                 const float t = div_(kp.lg_nn * (kp.lg_pn - comp<2>(ro)), n_dir);
                 const float u = (comp<XA>(ro) + comp<XA>(rd) * t - kp.lg_u0) * kp.lg_icw;
@@ -2282,14 +2299,24 @@ int needed_susp(const ipt_params* p) {
     return maxpush < 0 ? 0 : maxpush;  // suspended levels = depth of deepest pushed node
 }
 
+// dynamic LDS bytes of a path-kernel instance (the layout at the top of path_kernel)
+template <int MAXSUSP, int LMODE, int GEOM>
+size_t path_lds_bytes(const KParams& kp) {
+    constexpr int kBlock = block_of(LMODE);
+    const size_t cells = (size_t)kp.lg_nu * kp.lg_nv;
+    return ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
+            (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0) : 0) +
+            (grid_lights(LMODE) ? global_light_lds_words(kp.n_lights, 0, true) +
+                                      (lax_in_lds(LMODE) ? ((cells + 3) & ~(size_t)3) + 12 * (size_t)kp.n_lights : cells)
+                                : 0)) *
+           sizeof(float);
+}
+constexpr size_t kMaxLdsBytes = 160 * 1024;  // per workgroup (and per CU) on gfx950
+
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
-    const size_t lds = ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
-                        (kp.cand_lds ? kLdsCand : 0) +
-                        (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0)
-                                                : 0) +
-                        (grid_lights(LMODE) ? global_light_lds_words(kp.n_lights, 0, true) + (size_t)kp.lg_nu * kp.lg_nv
-                                            : 0)) * sizeof(float);
+    constexpr int kBlock = block_of(LMODE);
+    const size_t lds = path_lds_bytes<MAXSUSP, LMODE, GEOM>(kp);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // persistent grid: every block the CUs can hold at once (a work queue, no
@@ -2334,10 +2361,18 @@ int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     if (kp.n_lights <= kLdsLights) return launch_path3<MAXSUSP, COUNT, kLightsLds>(ctx, kp, st);
     if constexpr (IPT_C2_ONLY == 0) {
         // (the lattice is only built for sphere-in-box scenes)
-        if (ctx->lgrid.pattern == 1 && kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX)
-            return launch_path4<MAXSUSP, COUNT, kLightsGridA10, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
-        if (ctx->lgrid.pattern == 2 && kp.geometry_kind == IPT_GEOM_SPHERE_IN_BOX)
-            return launch_path4<MAXSUSP, COUNT, kLightsGridA01, IPT_GEOM_SPHERE_IN_BOX>(ctx, kp, st);
+        // the records-in-LDS instance wherever its LDS fits one workgroup per CU
+        constexpr int G = IPT_GEOM_SPHERE_IN_BOX;
+        if (ctx->lgrid.pattern == 1 && kp.geometry_kind == G) {
+            if (IPT_LAX_LDS && path_lds_bytes<MAXSUSP, kLightsGridA10L, G>(kp) <= kMaxLdsBytes)
+                return launch_path4<MAXSUSP, COUNT, kLightsGridA10L, G>(ctx, kp, st);
+            return launch_path4<MAXSUSP, COUNT, kLightsGridA10, G>(ctx, kp, st);
+        }
+        if (ctx->lgrid.pattern == 2 && kp.geometry_kind == G) {
+            if (IPT_LAX_LDS && path_lds_bytes<MAXSUSP, kLightsGridA01L, G>(kp) <= kMaxLdsBytes)
+                return launch_path4<MAXSUSP, COUNT, kLightsGridA01L, G>(ctx, kp, st);
+            return launch_path4<MAXSUSP, COUNT, kLightsGridA01, G>(ctx, kp, st);
+        }
     }
     return launch_path3<MAXSUSP, COUNT, kLightsGlobal>(ctx, kp, st);
 }
@@ -2469,7 +2504,6 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cos_a = ctx->d_cos_a;
         kp.cos_b = ctx->d_cos_b;
         kp.frame_sc = ctx->d_frame_sc;
-        kp.cand_lds = (p->n_shards > 1 && p->tile_rows > 0 && kp.n_cand <= kLdsCand) ? 1 : 0;
         kp.rg = ctx->d_rg;
         kp.count = count ? 1 : 0;
         HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));

@@ -11,7 +11,7 @@
      defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
-     defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || \
+     defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE))
 #error "an ipt_knobs.h parameter is overridden: A/B builds must define IPT_AB_BUILD"
@@ -64,6 +64,9 @@
 #endif
 #ifndef IPT_LIGHT_AX_REC
 #define IPT_LIGHT_AX_REC 1  // lattice lights read from 48-byte compact records (three 16-byte loads)
+#endif
+#ifndef IPT_LAX_LDS
+#define IPT_LAX_LDS 1  // lattice lights' records in LDS, one 1024-thread workgroup per CU (C5 +5 %)
 #endif
 #ifndef IPT_CDF_LO
 #define IPT_CDF_LO 1  // many lights: the pick's scan started from a 256-bucket table (+7 % C5)
