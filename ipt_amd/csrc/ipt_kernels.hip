@@ -80,6 +80,11 @@ struct KParams {
     const int* __restrict__ grid_start;   // [cells + 1]
     const GridCell* __restrict__ grid_cells;  // [cells] range + first three items (IPT_GRID_INLINE)
     const BvhSphere* __restrict__ grid_items;
+    // the same items packed for the pipelined walk (IPT_GRID_C4): centre and
+    // radius as one float4 per item (16-byte stride: a cell's items share
+    // lines), original indices in a separate array
+    const float4* __restrict__ grid_c4;
+    const int* __restrict__ grid_idx;
     const BvhNode* __restrict__ bvh_nodes;     // n_nodes > 0: sphere BVH (ipt_bvh.h)
     const BvhSphere* __restrict__ bvh_prims;
     int n_nodes;
@@ -281,6 +286,14 @@ __device__ __forceinline__ void sphere_grid_init(const KParams& kp, vec3 o, vec3
     cell = ia[0] | ia[1] << 8 | ia[2] << 16;
     tmx = v3(tm[0], tm[1], tm[2]);
 }
+__device__ __forceinline__ float4 grid_item(const KParams& kp, int k) {
+    if constexpr (IPT_GRID_C4) return kp.grid_c4[k];
+    return *reinterpret_cast<const float4*>(kp.grid_items[k].c);
+}
+__device__ __forceinline__ int grid_item_index(const KParams& kp, int k) {
+    if constexpr (IPT_GRID_C4) return kp.grid_idx[k];
+    return kp.grid_items[k].index;
+}
 // POS (the pipelined walk of the resumable instances, IPT_GRID_PIPE): bidx is
 // the best item's position in grid_items instead of its original index, so an
 // item is one 16-byte load and its index is read only on a tie (the caller
@@ -429,7 +442,7 @@ __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3
                 if (isfinite_(t) && gt_1em6(fabs_(t))) {
                     if (t < best)
                         bidx = k2;
-                    else if (t == best && bidx >= 0 && kp.grid_items[k2].index < kp.grid_items[bidx].index)
+                    else if (t == best && bidx >= 0 && grid_item_index(kp, k2) < grid_item_index(kp, bidx))
                         bidx = k2;
                     best = t < best ? t : best;
                 }
@@ -439,7 +452,7 @@ __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3
                     float4 c4[X];
 #pragma unroll
                     for (int q = 0; q < X; ++q)
-                        c4[q] = *reinterpret_cast<const float4*>(kp.grid_items[k2 + q < s1 ? k2 + q : k2].c);
+                        c4[q] = grid_item(kp, k2 + q < s1 ? k2 + q : k2);
                     test(c4[0], k2);
 #pragma unroll
                     for (int q = 1; q < X; ++q)
@@ -1697,7 +1710,7 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
             if (done) {
                 tracing = false;
                 if (IPT_GRID_PIPE && kp.n_grid > 0 && xbidx >= 0)
-                    xbidx = kg.grid_items[xbidx].index;  // item position -> original index
+                    xbidx = grid_item_index(kg, xbidx);  // item position -> original index
                 resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : xp, xro, xrd, xrdepth, xis_iter, xmult, xhas_li, xli_pos,
                         xli_pow);
             }
@@ -2114,8 +2127,10 @@ struct ipt_ctx {
     float bvh_tmargin = 0.0f;  // sphere BVH pruning margin (ipt_bvh.h)
     SphereGrid grid;           // geometry of the uniform sphere grid (host copy)
     int n_grid = 0;
+    size_t grid_n_items = 0;
     int* d_grid_start = nullptr;
     BvhSphere* d_grid_items = nullptr;
+    float4* d_grid_c4 = nullptr;  // [items] centre/radius, then [items] original indices
     GridCell* d_grid_cells = nullptr;  // 64-byte cell records (IPT_GRID_INLINE)
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
@@ -2480,6 +2495,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.grid_m = ctx->grid.m;
         kp.grid_start = ctx->d_grid_start;
         kp.grid_items = ctx->d_grid_items;
+        kp.grid_c4 = ctx->d_grid_c4;
+        kp.grid_idx = ctx->d_grid_c4 ? reinterpret_cast<const int*>(ctx->d_grid_c4 + ctx->grid_n_items) : nullptr;
         kp.grid_cells = ctx->d_grid_cells;
         kp.bvh_prims = ctx->d_bvh_prims;
         kp.n_nodes = ctx->n_nodes;
@@ -2623,7 +2640,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_lax, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
                     ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
-                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_frame_sc};
+                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_frame_sc};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (auto& e : ctx->ev)
@@ -2768,6 +2785,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     DevBuf<int> n_grid_start, n_lgrid, n_cdf_lo;
     DevBuf<LightAx> n_lax;
     DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
+    DevBuf<float4> n_grid_c4;
     DevBuf<GridCell> n_grid_cells;
     DevBuf<BvhNode> n_light_nodes, n_bvh_nodes;
     DevBuf<LightDev> n_lights;
@@ -2777,6 +2795,17 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     int rc = IPT_OK;
     if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
     if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
+    if (IPT_GRID_C4 && use_grid && !rc) {
+        const size_t ni = grid.items.size();
+        std::vector<float4> c4(ni + (ni + 3) / 4);
+        int* idx = reinterpret_cast<int*>(c4.data() + ni);
+        for (size_t k = 0; k < ni; ++k) {
+            const BvhSphere& b = grid.items[k];
+            c4[k] = make_float4(b.c[0], b.c[1], b.c[2], b.r);
+            idx[k] = b.index;
+        }
+        rc = upload(n_grid_c4, c4.data(), c4.size());
+    }
     std::vector<GridCell> gcells;
     if (IPT_GRID_INLINE && use_grid) grid_cells_build(grid, gcells);
     if (IPT_GRID_INLINE && use_grid && !rc) rc = upload(n_grid_cells, gcells.data(), gcells.size());
@@ -2796,16 +2825,18 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!rc) rc = upload(n_spheres, sph.data(), sph.size());
     if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
-                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_cells, ctx->d_wall, ctx->d_lgrid, ctx->d_lax,
+                   ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_wall, ctx->d_lgrid, ctx->d_lax,
                    ctx->d_cdf_lo};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_grid_start = n_grid_start.release();
     ctx->d_grid_items = n_grid_items.release();
+    ctx->d_grid_c4 = n_grid_c4.release();
     ctx->d_grid_cells = n_grid_cells.release();
     ctx->n_grid = 0;
     if (use_grid) {
         ctx->n_grid = (int)(grid.start.size() - 1);
+        ctx->grid_n_items = grid.items.size();
         ctx->bvh_tmargin = grid.tmargin;
         grid.start.clear();
         grid.items.clear();

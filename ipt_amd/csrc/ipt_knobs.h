@@ -8,7 +8,7 @@
 
 #if !defined(IPT_AB_BUILD) &&                                                                           \
     (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
-     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
+     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
@@ -67,6 +67,9 @@
 #endif
 #ifndef IPT_LAX_LDS
 #define IPT_LAX_LDS 1  // lattice lights' records in LDS, one 1024-thread workgroup per CU (C5 +5 %)
+#endif
+#ifndef IPT_GRID_C4
+#define IPT_GRID_C4 1  // pipelined grid walk: items as packed 16-byte records, indices apart (C3 +1.5 %)
 #endif
 #ifndef IPT_CDF_LO
 #define IPT_CDF_LO 1  // many lights: the pick's scan started from a 256-bucket table (+7 % C5)
