@@ -183,7 +183,9 @@ const char* ipt_last_error(ipt_ctx* ctx); /* ctx may be NULL (creation errors) *
  * a tail where lanes have run out of paths, so batch passes per call).
  * Environment read here (diagnostics): IPT_LNODES_LDS=0 keeps the light BVH in
  * global memory, IPT_LIGHT_GRID=0 disables the light-lattice lookup (the light
- * BVH is used instead), IPT_BLOCKS_PER_CU caps the path kernel's residency. */
+ * BVH is used instead), IPT_LATTICE_LDS=0 keeps the lattice lights' records
+ * in global memory (256-thread workgroups instead of one 1024-thread
+ * workgroup per CU), IPT_BLOCKS_PER_CU caps the path kernel's residency. */
 int ipt_create(int hip_device, ipt_ctx** out);
 void ipt_destroy(ipt_ctx* ctx);
 

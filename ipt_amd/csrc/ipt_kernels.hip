@@ -2164,7 +2164,8 @@ struct ipt_ctx {
     float2* d_frame_sc = nullptr;  // frame_table_kernel (IPT_FRAME_TAB), 1 GiB
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
-    int blocks_per_cu = 0;
+    int blocks_per_cu = 0;      // of the last path-kernel launch
+    bool lattice_lds = true;    // IPT_LATTICE_LDS=0: the lattice instances with global records (tests)
 };
 
 namespace {
@@ -2379,12 +2380,12 @@ int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
         // the records-in-LDS instance wherever its LDS fits one workgroup per CU
         constexpr int G = IPT_GEOM_SPHERE_IN_BOX;
         if (ctx->lgrid.pattern == 1 && kp.geometry_kind == G) {
-            if (IPT_LAX_LDS && path_lds_bytes<MAXSUSP, kLightsGridA10L, G>(kp) <= kMaxLdsBytes)
+            if (IPT_LAX_LDS && ctx->lattice_lds && path_lds_bytes<MAXSUSP, kLightsGridA10L, G>(kp) <= kMaxLdsBytes)
                 return launch_path4<MAXSUSP, COUNT, kLightsGridA10L, G>(ctx, kp, st);
             return launch_path4<MAXSUSP, COUNT, kLightsGridA10, G>(ctx, kp, st);
         }
         if (ctx->lgrid.pattern == 2 && kp.geometry_kind == G) {
-            if (IPT_LAX_LDS && path_lds_bytes<MAXSUSP, kLightsGridA01L, G>(kp) <= kMaxLdsBytes)
+            if (IPT_LAX_LDS && ctx->lattice_lds && path_lds_bytes<MAXSUSP, kLightsGridA01L, G>(kp) <= kMaxLdsBytes)
                 return launch_path4<MAXSUSP, COUNT, kLightsGridA01L, G>(ctx, kp, st);
             return launch_path4<MAXSUSP, COUNT, kLightsGridA01, G>(ctx, kp, st);
         }
@@ -2618,6 +2619,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     if (const char* e = std::getenv("IPT_BLOCKS_PER_CU")) ctx->bpc_override = std::atoi(e);  // profiling only
     if (const char* e = std::getenv("IPT_LNODES_LDS")) ctx->lnodes_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("IPT_LIGHT_GRID")) ctx->light_grid_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("IPT_LATTICE_LDS")) ctx->lattice_lds = std::atoi(e) != 0;
     if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return fail(nullptr, IPT_E_DEVICE, "stream creation failed");

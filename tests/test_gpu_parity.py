@@ -239,6 +239,28 @@ def test_light_grid_bit_exact(gpu_ctx, oracle, k):
     assert np.array_equal(_bits(gv), _bits(ov)), int((_bits(gv) != _bits(ov)).sum())
 
 
+@pytest.mark.parametrize("k", [8, 16])
+def test_light_grid_lds_and_global_records_bit_exact(oracle, monkeypatch, k):
+    """The lattice instances with the records in LDS (one 1024-thread workgroup
+    per CU, the default where the LDS fits) and in global memory
+    (IPT_LATTICE_LDS=0, 256-thread workgroups) give the same bits as the
+    oracle, at depth 8 / 16 rays (C5's stack depth)."""
+    desc = scenes.make_scene_box_lights(k)
+    p = capi.make_params(24, 16, 2, n_rays=16, depth_max=8)
+    out = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("IPT_LATTICE_LDS", lds)
+        ctx = capi.Context(0)
+        try:
+            gv, gc, ov, oc = _render_both(ctx, desc, p, oracle)
+        finally:
+            ctx.close()
+        assert np.array_equal(gc, oc)
+        assert np.array_equal(_bits(gv), _bits(ov)), (lds, int((_bits(gv) != _bits(ov)).sum()))
+        out.append(gv)
+    assert np.array_equal(_bits(out[0]), _bits(out[1]))
+
+
 @pytest.mark.parametrize("variant", ["nudged", "gap", "mixed_axes"])
 def test_light_grid_fallback_bit_exact(gpu_ctx, oracle, variant):
     """Light sets that are not a lattice (one emitter moved by a tenth of a
