@@ -513,6 +513,307 @@ __device__ __forceinline__ void sphere_grid_walk(const KParams& kp, vec3 o, vec3
     }
 }
 
+// Wave-wide inclusive scans over the 64 lanes (DPP: row shifts within each
+// 16-lane row, then rows 1/3 from lane 15 of the row before and rows 2/3 from
+// lane 31). Called with every lane of the wave active.
+__device__ __forceinline__ int wave_scan_add(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ int wave_scan_max(int v) {  // v >= 0
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+// Orders one wave's LDS accesses across its lanes for the compiler (the
+// hardware runs a wave's LDS instructions in order): without it a lane's load
+// of a word it stored itself would be forwarded from that store, missing the
+// other lanes' stores in between.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The resumable grid walk with the item tests spread over the whole wave
+// (IPT_GRID_WAVE). Per wave iteration every walking lane steps one cell: the
+// (lane, item) pairs of the cells the lanes stand on are numbered by a wave
+// prefix sum and tested 64 at a time, one pair per lane (the lane that owns
+// pair p is found from a 64-byte LDS table of segment starts and a max-scan;
+// its ray is read with ds_bpermute), and each accepted t goes to its owner's
+// LDS slot as an atomic minimum of (t bits << 32 | item position). Within a
+// cell the positions are in original-index order (grid_build_spheres fills
+// each cell in index order) and accepted t are positive, so the slot ends as
+// the cell's (t, index) minimum; the owner merges it with `accept`, the
+// per-lane walk's rule (FractalSpheres.cpp:75-84: strict '<', lowest index on
+// equal t, a plane never loses a tie). The tests run at full lane
+// utilisation instead of once per lane per item slot. Same cells, same tests
+// (sphere_t on the same operands), same exit decisions: the (t, index) minimum
+// does not depend on the order of the tests. Every lane of the wave calls it.
+template <bool COUNT>
+__device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool walking, vec3 o, vec3 d, int& cell,
+                                                      vec3& tmx, float& best, int& bidx, int budget,
+                                                      unsigned long long* slots, uint8_t* own, int lane,
+                                                      uint32_t& c_nodes, uint32_t& c_tests) {
+    const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    auto lin_of = [&](int c) {
+        return (c & 0xff) + kp.grid_n[0] * (((c >> 8) & 0xff) + kp.grid_n[1] * (c >> 16));
+    };
+    bool act = walking && cell >= 0 && budget > 0;
+    int lin = 0, s0 = 0, s1 = 0;
+    if (act) {
+        lin = lin_of(cell);
+        s0 = kp.grid_start[lin];
+        s1 = kp.grid_start[lin + 1];
+    }
+    for (int it = 0;; ++it) {
+        // (after IPT_GRID_WAVE_FLOOR_IT iterations the wave stops once fewer than
+        // IPT_GRID_WAVE_FLOOR lanes walk; they resume in the next step)
+        const uint64_t am = __ballot(act);
+        if (!am || (it >= IPT_GRID_WAVE_FLOOR_IT && __popcll(am) < IPT_GRID_WAVE_FLOOR)) break;
+        // the next cell (from tmx alone) and its range, in flight during the tests
+        int ncell = 0, nlin = 0, n0 = 0, n1 = 0;
+        vec3 ntm = tmx;
+        bool nvalid = false;
+        if (act) {
+            const int ix = cell & 0xff, iy = (cell >> 8) & 0xff, iz = cell >> 16;
+            if (tmx.x <= tmx.y && tmx.x <= tmx.z) {
+                const int nx = d.x > 0.0f ? ix + 1 : ix - 1;
+                nvalid = !(nx < 0 || nx >= kp.grid_n[0]);
+                ncell = (cell & ~0xff) | (nx & 0xff);
+                ntm.x = ((kp.grid_g0[0] + (float)(d.x > 0.0f ? nx + 1 : nx) * kp.grid_h[0]) - o.x) * inv.x;
+            } else if (tmx.y <= tmx.z) {
+                const int ny = d.y > 0.0f ? iy + 1 : iy - 1;
+                nvalid = !(ny < 0 || ny >= kp.grid_n[1]);
+                ncell = (cell & ~0xff00) | (ny & 0xff) << 8;
+                ntm.y = ((kp.grid_g0[1] + (float)(d.y > 0.0f ? ny + 1 : ny) * kp.grid_h[1]) - o.y) * inv.y;
+            } else {
+                const int nz = d.z > 0.0f ? iz + 1 : iz - 1;
+                nvalid = !(nz < 0 || nz >= kp.grid_n[2]);
+                ncell = (cell & 0xffff) | (nz & 0xff) << 16;
+                ntm.z = ((kp.grid_g0[2] + (float)(d.z > 0.0f ? nz + 1 : nz) * kp.grid_h[2]) - o.z) * inv.z;
+            }
+            nlin = nvalid ? lin_of(ncell) : lin;
+            n0 = kp.grid_start[nlin];
+            n1 = kp.grid_start[nlin + 1];
+        }
+        const int cnt = act ? s1 - s0 : 0;
+        if (COUNT && act) {
+            ++c_nodes;
+            c_tests += (uint32_t)cnt;
+        }
+        const int incl = wave_scan_add(cnt);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        const int excl = incl - cnt;
+        if (total > 0) {
+            if (cnt > 0) slots[lane] = ~0ull;
+            const int dk = s0 - excl;  // pair p of this lane tests item p + dk
+            for (int base = 0; base < total; base += 64) {
+                own[lane] = 0;
+                if (cnt > 0 && excl < base + 64 && incl > base) own[excl > base ? excl - base : 0] = (uint8_t)(lane + 1);
+                wave_lds_sync();
+                const int src = wave_scan_max((int)own[lane]) - 1;
+                const int p = base + lane;
+                const bool valid = p < total;
+                const int sl = valid ? src : lane;
+                const float ox = __shfl(o.x, sl), oy = __shfl(o.y, sl), oz = __shfl(o.z, sl);
+                const float dx = __shfl(d.x, sl), dy = __shfl(d.y, sl), dz = __shfl(d.z, sl);
+                const int k = p + __shfl(dk, sl);
+                if (valid) {
+                    const float4 c4 = grid_item(kp, k);
+                    const float t = sphere_t(c4.w, v3(ox, oy, oz) - v3(c4.x, c4.y, c4.z), v3(dx, dy, dz));
+                    if (isfinite_(t) && gt_1em6(fabs_(t)))
+                        __hip_atomic_fetch_min(slots + src,
+                                               (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)k,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+            }
+            wave_lds_sync();
+            if (cnt > 0) {
+                const unsigned long long key = slots[lane];
+                if (key != ~0ull) {
+                    const float t = __uint_as_float((uint32_t)(key >> 32));
+                    const int k2 = (int)(uint32_t)key;
+                    if (t < best)
+                        bidx = k2;
+                    else if (t == best && bidx >= 0 && grid_item_index(kp, k2) < grid_item_index(kp, bidx))
+                        bidx = k2;
+                    best = t < best ? t : best;
+                }
+            }
+        }
+        if (act) {
+            --budget;
+            const float texit = fminf(fminf(tmx.x, tmx.y), tmx.z);
+            if (texit > (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f || !nvalid) {
+                cell = -1;
+                act = false;
+            } else {
+                cell = ncell;
+                tmx = ntm;
+                lin = nlin;
+                s0 = n0;
+                s1 = n1;
+                act = budget > 0;
+            }
+        }
+    }
+}
+
+// IPT_GRID_WAVE == 2: the same with two cells per lane per wave iteration --
+// the cell the lane stands on (A) and the next one (B), whose range was
+// fetched in the previous iteration; the two cells after them are located and
+// their ranges fetched while A's and B's items are tested -- and the slots
+// keyed by (t bits << 32 | original index) (the index is loaded with the
+// item), so bidx holds the original index and the minimum over two cells'
+// items is the scan's (t, index) rule directly. Exit tests after A and after
+// B as in the per-cell walk; B's items are tested even when the walk ends
+// after A, which is harmless (any sphere's t is a valid candidate of the
+// scan, and the exit bound only shrinks with best). Two cells of budget per
+// iteration.
+template <bool COUNT>
+__device__ __forceinline__ void sphere_grid_walk_wave2(const KParams& kp, bool walking, vec3 o, vec3 d, int& cell,
+                                                       vec3& tmx, float& best, int& bidx, int budget,
+                                                       unsigned long long* slots, uint8_t* own, int lane,
+                                                       uint32_t& c_nodes, uint32_t& c_tests) {
+    const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    auto lin_of = [&](int c) {
+        return (c & 0xff) + kp.grid_n[0] * (((c >> 8) & 0xff) + kp.grid_n[1] * (c >> 16));
+    };
+    // one DDA step from cell c with boundary t's tm (ties: x, then y, then z)
+    auto step = [&](int c, vec3 tm, int& nc, vec3& ntm, bool& nv) {
+        const int ix = c & 0xff, iy = (c >> 8) & 0xff, iz = c >> 16;
+        ntm = tm;
+        if (tm.x <= tm.y && tm.x <= tm.z) {
+            const int nx = d.x > 0.0f ? ix + 1 : ix - 1;
+            nv = !(nx < 0 || nx >= kp.grid_n[0]);
+            nc = (c & ~0xff) | (nx & 0xff);
+            ntm.x = ((kp.grid_g0[0] + (float)(d.x > 0.0f ? nx + 1 : nx) * kp.grid_h[0]) - o.x) * inv.x;
+        } else if (tm.y <= tm.z) {
+            const int ny = d.y > 0.0f ? iy + 1 : iy - 1;
+            nv = !(ny < 0 || ny >= kp.grid_n[1]);
+            nc = (c & ~0xff00) | (ny & 0xff) << 8;
+            ntm.y = ((kp.grid_g0[1] + (float)(d.y > 0.0f ? ny + 1 : ny) * kp.grid_h[1]) - o.y) * inv.y;
+        } else {
+            const int nz = d.z > 0.0f ? iz + 1 : iz - 1;
+            nv = !(nz < 0 || nz >= kp.grid_n[2]);
+            nc = (c & 0xffff) | (nz & 0xff) << 16;
+            ntm.z = ((kp.grid_g0[2] + (float)(d.z > 0.0f ? nz + 1 : nz) * kp.grid_h[2]) - o.z) * inv.z;
+        }
+    };
+    bool act = walking && cell >= 0 && budget > 0;
+    int s0 = 0, s1 = 0, cb = 0, a0 = 0, a1 = 0;
+    vec3 tmb = tmx;
+    bool bval = false;
+    if (act) {
+        const int l = lin_of(cell);
+        s0 = kp.grid_start[l];
+        s1 = kp.grid_start[l + 1];
+        step(cell, tmx, cb, tmb, bval);
+        if (bval) {
+            const int lb = lin_of(cb);
+            a0 = kp.grid_start[lb];
+            a1 = kp.grid_start[lb + 1];
+        }
+    }
+    while (__ballot(act)) {
+        // cells C and D after A, B and their ranges, in flight during the tests
+        int cc = 0, cd = 0, c0 = 0, c1 = 0, d0 = 0, d1 = 0;
+        vec3 tmc = tmb, tmd = tmb;
+        bool cval = false, dval = false;
+        if (act && bval) {
+            step(cb, tmb, cc, tmc, cval);
+            if (cval) {
+                const int lc = lin_of(cc);
+                c0 = kp.grid_start[lc];
+                c1 = kp.grid_start[lc + 1];
+                step(cc, tmc, cd, tmd, dval);
+                if (dval) {
+                    const int ld = lin_of(cd);
+                    d0 = kp.grid_start[ld];
+                    d1 = kp.grid_start[ld + 1];
+                }
+            }
+        }
+        const int cnta = act ? s1 - s0 : 0;
+        const int cnt = cnta + ((act && bval) ? a1 - a0 : 0);
+        if (COUNT && act) {
+            c_nodes += bval ? 2u : 1u;
+            c_tests += (uint32_t)cnt;
+        }
+        const int incl = wave_scan_add(cnt);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        const int excl = incl - cnt;
+        if (total > 0) {
+            if (cnt > 0) slots[lane] = ~0ull;
+            // pair p of this lane: item p + da (p < ea, cell A) or p + db (cell B)
+            const int ea = excl + cnta, da = s0 - excl, db = a0 - ea;
+            for (int base = 0; base < total; base += 64) {
+                own[lane] = 0;
+                if (cnt > 0 && excl < base + 64 && incl > base) own[excl > base ? excl - base : 0] = (uint8_t)(lane + 1);
+                wave_lds_sync();
+                const int src = wave_scan_max((int)own[lane]) - 1;
+                const int p = base + lane;
+                const bool valid = p < total;
+                const int sl = valid ? src : lane;
+                const float ox = __shfl(o.x, sl), oy = __shfl(o.y, sl), oz = __shfl(o.z, sl);
+                const float dx = __shfl(d.x, sl), dy = __shfl(d.y, sl), dz = __shfl(d.z, sl);
+                const int eao = __shfl(ea, sl), dao = __shfl(da, sl), dbo = __shfl(db, sl);
+                if (valid) {
+                    const int k = p < eao ? p + dao : p + dbo;
+                    const float4 c4 = kp.grid_c4[k];
+                    const int idx = kp.grid_idx[k];
+                    const float t = sphere_t(c4.w, v3(ox, oy, oz) - v3(c4.x, c4.y, c4.z), v3(dx, dy, dz));
+                    if (isfinite_(t) && gt_1em6(fabs_(t)))
+                        __hip_atomic_fetch_min(slots + src,
+                                               (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)idx,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+            }
+            wave_lds_sync();
+            if (cnt > 0) {
+                const unsigned long long key = slots[lane];
+                if (key != ~0ull) {
+                    const float t = __uint_as_float((uint32_t)(key >> 32));
+                    const int idx = (int)(uint32_t)key;
+                    if (t < best || (t == best && bidx >= 0 && idx < bidx)) bidx = idx;
+                    best = t < best ? t : best;
+                }
+            }
+        }
+        if (act) {
+            budget -= 2;
+            const float bound = (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f;
+            if (fminf(fminf(tmx.x, tmx.y), tmx.z) > bound || !bval || fminf(fminf(tmb.x, tmb.y), tmb.z) > bound ||
+                !cval) {
+                cell = -1;
+                act = false;
+            } else {
+                cell = cc;
+                tmx = tmc;
+                s0 = c0;
+                s1 = c1;
+                cb = cd;
+                tmb = tmd;
+                bval = dval;
+                a0 = d0;
+                a1 = d1;
+                act = budget > 0;
+            }
+        }
+    }
+}
+
 // Nearest geometry hit for both geometry kinds. prim: 0..4 plane, 5 the
 // r=0.5 sphere, 6+i extra sphere i (original index), -1 miss.
 template <bool COUNT, int GEOM>
@@ -618,11 +919,17 @@ constexpr int kLatticeBlock = 1024;
 __host__ __device__ constexpr int block_of(int lmode) {
     return (lmode == 9 || lmode == 10) ? kLatticeBlock : kBlock;
 }
-__host__ __device__ constexpr int frame_stride(int lmode) {
-    return (lmode == 1 || lmode == 5 || lmode == 6) ? block_of(lmode) + 64 : block_of(lmode) + 8;
+__host__ __device__ constexpr bool resumable_geom(int geom);
+// the wave-spread grid walk's per-lane LDS (IPT_GRID_WAVE): 8-byte slot + 1 byte
+__host__ __device__ constexpr int walk_lds_words(int lmode, int geom) {
+    return (IPT_GRID_WAVE && resumable_geom(geom)) ? 2 * block_of(lmode) + block_of(lmode) / 4 : 0;
+}
+__host__ __device__ constexpr int frame_stride(int lmode, int geom) {
+    return ((lmode == 1 || lmode == 5 || lmode == 6) && walk_lds_words(lmode, geom) == 0) ? block_of(lmode) + 64
+                                                                                        : block_of(lmode) + 8;
 }
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
-    return 12 * (size_t)frame_stride(lmode) +
+    return (size_t)walk_lds_words(lmode, geom) + 12 * (size_t)frame_stride(lmode, geom) +
            (lmode == 2 ? (size_t)kLdsLights * kLightWords + 2 * (kLdsLights + 1) : 0);
 }
 // kLightsGlobal: mixture weights + CDF (and, when small, the light BVH) are
@@ -780,9 +1087,13 @@ template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
     constexpr int kBlock = block_of(LMODE);  // this instance's workgroup size
     extern __shared__ float lds[];
-    float* stk = lds;                                         // [MAXSUSP][F][kBlock]
-    constexpr int kFrameStride = frame_stride(LMODE);
-    float* lfr = lds + MAXSUSP * kStackFields * kBlock;       // [12][kFrameStride] lane + wall frames
+    // IPT_GRID_WAVE (resumable sphere-list instances): a 64-bit test slot and a
+    // segment-start byte per lane in front of the stack
+    unsigned long long* wslots = reinterpret_cast<unsigned long long*>(lds);
+    uint8_t* wown = reinterpret_cast<uint8_t*>(lds + 2 * kBlock);
+    float* stk = lds + walk_lds_words(LMODE, GEOM);           // [MAXSUSP][F][kBlock]
+    constexpr int kFrameStride = frame_stride(LMODE, GEOM);
+    float* lfr = stk + MAXSUSP * kStackFields * kBlock;       // [12][kFrameStride] lane + wall frames
     LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride);
     float* weights_lds = reinterpret_cast<float*>(lights_lds) + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
@@ -1696,7 +2007,23 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
             }
         }
         IPT_STAMP_AT(11);  // resolve + push
-        if (kRes && tracing) {
+        if (kRes && IPT_GRID_WAVE && kp.n_grid > 0) {
+            // the whole wave walks (the item tests are spread over its lanes)
+            if (__ballot(tracing)) {
+                if constexpr (IPT_GRID_WAVE == 2)
+                    sphere_grid_walk_wave2<COUNT>(kg, tracing, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
+                                                  wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes, c_tests);
+                else
+                    sphere_grid_walk_wave<COUNT>(kg, tracing, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
+                                                 wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes, c_tests);
+            }
+            if (tracing && xi < 0) {
+                tracing = false;
+                if (IPT_GRID_WAVE != 2 && xbidx >= 0) xbidx = grid_item_index(kg, xbidx);  // item position -> original index
+                resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : xp, xro, xrd, xrdepth, xis_iter, xmult, xhas_li, xli_pos,
+                        xli_pow);
+            }
+        } else if (kRes && tracing) {
             IPT_PHASE(9);
             bool done;
             if (kp.n_grid > 0) {
