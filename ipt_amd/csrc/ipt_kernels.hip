@@ -618,25 +618,50 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
         if (total > 0) {
             if (cnt > 0) slots[lane] = ~0ull;
             const int dk = s0 - excl;  // pair p of this lane tests item p + dk
-            for (int base = 0; base < total; base += 64) {
+            // one round: pairs base .. base + 63 (owner, its ray, the item)
+            struct Pair {
+                vec3 o, d;
+                float4 c4;
+                int k, src;
+                bool valid;
+            };
+            auto setup = [&](int base, Pair& q) {
                 own[lane] = 0;
                 if (cnt > 0 && excl < base + 64 && incl > base) own[excl > base ? excl - base : 0] = (uint8_t)(lane + 1);
                 wave_lds_sync();
-                const int src = wave_scan_max((int)own[lane]) - 1;
+                q.src = wave_scan_max((int)own[lane]) - 1;
                 const int p = base + lane;
-                const bool valid = p < total;
-                const int sl = valid ? src : lane;
-                const float ox = __shfl(o.x, sl), oy = __shfl(o.y, sl), oz = __shfl(o.z, sl);
-                const float dx = __shfl(d.x, sl), dy = __shfl(d.y, sl), dz = __shfl(d.z, sl);
-                const int k = p + __shfl(dk, sl);
-                if (valid) {
-                    const float4 c4 = grid_item(kp, k);
-                    const float t = sphere_t(c4.w, v3(ox, oy, oz) - v3(c4.x, c4.y, c4.z), v3(dx, dy, dz));
+                q.valid = p < total;
+                const int sl = q.valid ? q.src : lane;
+                q.o = v3(__shfl(o.x, sl), __shfl(o.y, sl), __shfl(o.z, sl));
+                q.d = v3(__shfl(d.x, sl), __shfl(d.y, sl), __shfl(d.z, sl));
+                q.k = p + __shfl(dk, sl);
+                if (q.valid) q.c4 = grid_item(kp, q.k);
+            };
+            auto test = [&](const Pair& q) {
+                if (q.valid) {
+                    const float t = sphere_t(q.c4.w, q.o - v3(q.c4.x, q.c4.y, q.c4.z), q.d);
                     if (isfinite_(t) && gt_1em6(fabs_(t)))
-                        __hip_atomic_fetch_min(slots + src,
-                                               (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)k,
+                        __hip_atomic_fetch_min(slots + q.src,
+                                               (unsigned long long)__float_as_uint(t) << 32 | (uint32_t)q.k,
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
                 }
+            };
+            int base = 0;
+            if constexpr (IPT_GRID_WAVE_PIPE) {
+                // the first two rounds' items fetched together
+                Pair q0, q1;
+                setup(0, q0);
+                const bool two = total > 64;
+                if (two) setup(64, q1);
+                test(q0);
+                if (two) test(q1);
+                base = 128;
+            }
+            for (; base < total; base += 64) {
+                Pair q;
+                setup(base, q);
+                test(q);
             }
             wave_lds_sync();
             if (cnt > 0) {
@@ -1549,7 +1574,10 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                 // (its own range checks; a normalized `to`), exact fallback
                 const vec3 to = normalize(nrm);
                 float fs, fc;
-                frame_angle_sc(to, &fs, &fc);
+                if (IPT_FRAME_TAB && IPT_FRAME_TAB_LISTS && GEOM == IPT_GEOM_SPHERES_IN_BOX)
+                    frame_sc_lookup(kp.frame_sc, to, fs, fc);
+                else
+                    frame_angle_sc(to, &fs, &fc);
                 bool ok;
                 f = make_frame_sc_fast(to, fs, fc, ok);
                 if (__builtin_expect(__any(!ok), 0))
@@ -2534,6 +2562,10 @@ int ensure_cos_tables(ipt_ctx* ctx, hipStream_t st) {
     return IPT_OK;
 }
 
+// the geometries whose sphere-node frames read the frame-angle table
+constexpr bool frame_table_user(int geom) {
+    return geom == IPT_GEOM_SPHERE_IN_BOX || (IPT_FRAME_TAB_LISTS && geom == IPT_GEOM_SPHERES_IN_BOX);
+}
 int ensure_frame_table(ipt_ctx* ctx, hipStream_t st) {
     if (!IPT_FRAME_TAB || ctx->d_frame_sc) return IPT_OK;
     DevBuf<float2> t;
@@ -2749,7 +2781,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             size_t avail = free_b + ctx->work_cap * kUnitBytes;
             const size_t tables = (ctx->d_cos_a ? 0 : ((size_t)3 << 26)) +
-                                  (ctx->d_frame_sc || ctx->geometry_kind != IPT_GEOM_SPHERE_IN_BOX
+                                  (ctx->d_frame_sc || !frame_table_user(ctx->geometry_kind)
                                        ? 0 : kFrameTabEntries * sizeof(float2));
             avail = avail > tables ? avail - tables : 0;
             budget = std::min(budget, std::max<size_t>(per_pass, avail / 4 * 3 / kUnitBytes));
@@ -2762,7 +2794,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     if (rc) return rc;
     rc = ensure_cos_tables(ctx, st);
     if (rc) return rc;
-    if (ctx->geometry_kind == IPT_GEOM_SPHERE_IN_BOX) {  // its only user (path_kernel)
+    if (frame_table_user(ctx->geometry_kind)) {  // path_kernel's frame builds
         rc = ensure_frame_table(ctx, st);
         if (rc) return rc;
     }

@@ -8,11 +8,11 @@
 
 #if !defined(IPT_AB_BUILD) &&                                                                           \
     (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
-     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
+     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
-     defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
+     defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE))
 #error "an ipt_knobs.h parameter is overridden: A/B builds must define IPT_AB_BUILD"
 #endif
@@ -41,6 +41,9 @@
 #endif
 #ifndef IPT_FRAME_TAB
 #define IPT_FRAME_TAB 1  // RotateDdf angle (sin, cos) from the exact 1 GiB frame table (+8.6 % C2)
+#endif
+#ifndef IPT_FRAME_TAB_LISTS
+#define IPT_FRAME_TAB_LISTS 0  // ... for the sphere-list (C3) frames too
 #endif
 #ifndef IPT_FRAME_PF
 #define IPT_FRAME_PF 3  // 3: the next step's frame-table entry gathered at the end of the step
@@ -89,6 +92,9 @@
 
 #ifndef IPT_GRID_WAVE
 #define IPT_GRID_WAVE 1  // resumable grid walk with the item tests spread over the wave's lanes (C3 +14 %)
+#endif
+#ifndef IPT_GRID_WAVE_PIPE
+#define IPT_GRID_WAVE_PIPE 0  // ... with the first two rounds' item loads issued together
 #endif
 #ifndef IPT_GRID_WAVE_FLOOR
 #define IPT_GRID_WAVE_FLOOR 0  // ... ended early once fewer lanes than this walk
