@@ -317,9 +317,36 @@ inline bool grid_build_spheres(const float* cr, int n, const float cam[3], float
         for (int i = 0; i < n; ++i) {
             int r0[3], r1[3];
             for (int a = 0; a < 3; ++a) range(a, lo[3 * (size_t)i + a], hi[3 * (size_t)i + a], &r0[a], &r1[a]);
+            // IPT_GRID_SPHERE_REG: of the padded box's cells, only those within
+            // the padded sphere's reach (the box is that sphere's bound: its
+            // half-width pad + r enlarges the radius), inflated by m plus a
+            // rounding allowance, in double
+            double cc[3], reach2 = 0.0;
+            if (IPT_GRID_SPHERE_REG) {
+                double rr = 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    cc[a] = 0.5 * (lo[3 * (size_t)i + a] + hi[3 * (size_t)i + a]);
+                    rr = std::max(rr, 0.5 * (hi[3 * (size_t)i + a] - lo[3 * (size_t)i + a]));
+                }
+                // + the box centre's offset from the float centre (fl(c -+ r) roundings)
+                const double reach = (rr + m + 1e-6 * (1.0 + std::fabs(cc[0]) + std::fabs(cc[1]) + std::fabs(cc[2]))) *
+                                     (1.0 + 1e-9);
+                reach2 = reach * reach;
+            }
             for (int z = r0[2]; z <= r1[2]; ++z)
                 for (int y = r0[1]; y <= r1[1]; ++y)
                     for (int x = r0[0]; x <= r1[0]; ++x) {
+                        if (IPT_GRID_SPHERE_REG) {
+                            const int xyz[3] = {x, y, z};
+                            double d2 = 0.0;
+                            for (int a = 0; a < 3; ++a) {
+                                const double c0 = (double)g.g0[a] + (double)xyz[a] * (double)g.h[a];
+                                const double c1 = (double)g.g0[a] + (double)(xyz[a] + 1) * (double)g.h[a];
+                                const double dd = cc[a] < c0 ? c0 - cc[a] : (cc[a] > c1 ? cc[a] - c1 : 0.0);
+                                d2 += dd * dd;
+                            }
+                            if (d2 > reach2) continue;
+                        }
                         const size_t c = (size_t)x + (size_t)g.n[0] * ((size_t)y + (size_t)g.n[1] * z);
                         if (pass == 0) {
                             ++g.start[c + 1];

@@ -636,9 +636,18 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
                 q.o = v3(__shfl(o.x, sl), __shfl(o.y, sl), __shfl(o.z, sl));
                 q.d = v3(__shfl(d.x, sl), __shfl(d.y, sl), __shfl(d.z, sl));
                 q.k = p + __shfl(dk, sl);
-                if (q.valid) q.c4 = grid_item(kp, q.k);
+                if (IPT_GRID_WAVE_UNC)
+                    q.c4 = grid_item(kp, q.valid ? q.k : 0);
+                else if (q.valid)
+                    q.c4 = grid_item(kp, q.k);
             };
             auto test = [&](const Pair& q) {
+                // IPT_GRID_WAVE_UNC: every lane loads (item 0 for lanes without a
+                // pair) and the wave waits for the item here, outside the branch:
+                // otherwise a load left pending on the path that skips the test
+                // made the next round's load wait for every outstanding load,
+                // the next cell's range prefetch included (vmcnt(0))
+                if (IPT_GRID_WAVE_UNC) keep_alive(q.c4);
                 if (q.valid) {
                     const float t = sphere_t(q.c4.w, q.o - v3(q.c4.x, q.c4.y, q.c4.z), q.d);
                     if (isfinite_(t) && gt_1em6(fabs_(t)))

@@ -8,12 +8,12 @@
 
 #if !defined(IPT_AB_BUILD) &&                                                                           \
     (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
-     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
+     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
-     defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE))
+     defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG))
 #error "an ipt_knobs.h parameter is overridden: A/B builds must define IPT_AB_BUILD"
 #endif
 
@@ -93,6 +93,9 @@
 #ifndef IPT_GRID_WAVE
 #define IPT_GRID_WAVE 1  // resumable grid walk with the item tests spread over the wave's lanes (C3 +14 %)
 #endif
+#ifndef IPT_GRID_WAVE_UNC
+#define IPT_GRID_WAVE_UNC 0  // ... every lane loads an item per round, waited for outside the test's branch
+#endif
 #ifndef IPT_GRID_WAVE_PIPE
 #define IPT_GRID_WAVE_PIPE 0  // ... with the first two rounds' item loads issued together
 #endif
@@ -128,6 +131,10 @@
 #endif
 #ifndef IPT_GRID_CELLS_PER_SPHERE
 #define IPT_GRID_CELLS_PER_SPHERE 1.5  // C3 sweep: 0.75-12, best 1.5 with a 5-cell budget
+#endif
+
+#ifndef IPT_GRID_SPHERE_REG
+#define IPT_GRID_SPHERE_REG 0  // grid cells register a sphere only where its padded ball reaches them
 #endif
 
 // ---- experiment builds: -DIPT_AB_BUILD -DIPT_C2_ONLY=1 instantiates the
