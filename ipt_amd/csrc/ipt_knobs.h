@@ -94,7 +94,7 @@
 #define IPT_GRID_WAVE 1  // resumable grid walk with the item tests spread over the wave's lanes (C3 +14 %)
 #endif
 #ifndef IPT_GRID_WAVE_UNC
-#define IPT_GRID_WAVE_UNC 0  // ... every lane loads an item per round, waited for outside the test's branch
+#define IPT_GRID_WAVE_UNC 1  // ... every lane loads an item per round, waited for outside the test's branch
 #endif
 #ifndef IPT_GRID_WAVE_PIPE
 #define IPT_GRID_WAVE_PIPE 0  // ... with the first two rounds' item loads issued together
@@ -134,7 +134,7 @@
 #endif
 
 #ifndef IPT_GRID_SPHERE_REG
-#define IPT_GRID_SPHERE_REG 0  // grid cells register a sphere only where its padded ball reaches them
+#define IPT_GRID_SPHERE_REG 1  // grid cells register a sphere only where its padded ball reaches them
 #endif
 
 // ---- experiment builds: -DIPT_AB_BUILD -DIPT_C2_ONLY=1 instantiates the
