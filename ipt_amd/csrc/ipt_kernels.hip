@@ -570,9 +570,9 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
         return (c & 0xff) + kp.grid_n[0] * (((c >> 8) & 0xff) + kp.grid_n[1] * (c >> 16));
     };
     bool act = walking && cell >= 0 && budget > 0;
-    int lin = 0, s0 = 0, s1 = 0;
+    int s0 = 0, s1 = 0;
     if (act) {
-        lin = lin_of(cell);
+        const int lin = lin_of(cell);
         s0 = kp.grid_start[lin];
         s1 = kp.grid_start[lin + 1];
     }
@@ -582,7 +582,7 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
         const uint64_t am = __ballot(act);
         if (!am || (it >= IPT_GRID_WAVE_FLOOR_IT && __popcll(am) < IPT_GRID_WAVE_FLOOR)) break;
         // the next cell (from tmx alone) and its range, in flight during the tests
-        int ncell = 0, nlin = 0, n0 = 0, n1 = 0;
+        int ncell = 0, n0 = 0, n1 = 0;
         vec3 ntm = tmx;
         bool nvalid = false;
         if (act) {
@@ -603,7 +603,9 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
                 ncell = (cell & 0xffff) | (nz & 0xff) << 16;
                 ntm.z = ((kp.grid_g0[2] + (float)(d.z > 0.0f ? nz + 1 : nz) * kp.grid_h[2]) - o.z) * inv.z;
             }
-            nlin = nvalid ? lin_of(ncell) : lin;
+            ncell = nvalid ? ncell : -1;
+            // (no next cell: cell 0's range, unused)
+            const int nlin = nvalid ? lin_of(ncell) : 0;
             n0 = kp.grid_start[nlin];
             n1 = kp.grid_start[nlin + 1];
         }
@@ -689,13 +691,12 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
         if (act) {
             --budget;
             const float texit = fminf(fminf(tmx.x, tmx.y), tmx.z);
-            if (texit > (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f || !nvalid) {
+            if (texit > (best * 1.0001f + 1e-5f + kp.bvh_tmargin + kp.grid_m) * 1.00001f + 1e-5f || ncell < 0) {
                 cell = -1;
                 act = false;
             } else {
                 cell = ncell;
                 tmx = ntm;
-                lin = nlin;
                 s0 = n0;
                 s1 = n1;
                 act = budget > 0;
