@@ -347,7 +347,8 @@ def main():
                         and c0.get("depth_max", args.depth_max) == args.depth_max):
                     traffic = pm.get("path_kernel_hbm_bytes_per_launch")
                     occ = pm.get("path_kernel_occupancy")
-                    traffic_src = (f"profiles/{pm['tag']}_summary.json (rocprofv3 --pmc passes of the same "
+                    cfg_tag = f"_{pm['config_name']}" if pm.get("config_name") else ""
+                    traffic_src = (f"profiles/{pm['tag']}{cfg_tag}_summary.json (rocprofv3 --pmc passes of the same "
                                    f"config at N=1: FETCH_SIZE, WRITE_SIZE; SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE)")
                     break
             except Exception:
