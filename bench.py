@@ -45,13 +45,15 @@ sys.path.insert(0, str(ROOT))
 # BASELINE.json configs: scene, width, height, spp per step, steps, depth_max,
 # default scaling, CPU-baseline sample (row stride, column stride) per call.
 # c2's step is the whole 1024^2 x 256 spp frame (one launch of 268 M paths);
-# c3/c4/c5 sample their full spp counts with calls of 16.8 M / 537 M / 268 M
+# c3/c4/c5 sample their full spp counts with calls of 33.6 M / 537 M / 268 M
 # paths, so that the persistent kernel's end-of-launch tail (lanes out of
-# work while the longest paths finish) stays a small share of each launch.
+# work while the longest paths finish) stays a small share of each launch
+# (c3's two 32-spp steps are its whole 64-spp frame; at 16 spp per call the
+# tail cost it 6 %: 13.35 vs 14.23 Mpaths/s).
 CONFIGS = {
     "c1": ("box", 256, 256, 16, 1, 4, "weak", None),                 # configs[0]: CPU plumbing case
     "c2": ("box", 1024, 1024, 256, 2, 8, "weak", (64, 1)),           # configs[1]: the metric
-    "c3": ("spheres10k", 1024, 1024, 16, 2, 8, "strong", (128, 64)),  # configs[2]: 10k spheres (64 spp in full)
+    "c3": ("spheres10k", 1024, 1024, 32, 2, 8, "strong", (128, 64)),  # configs[2]: 10k spheres, 2 steps = the 64-spp frame
     "c4": ("box", 4096, 4096, 32, 2, 8, "strong", (256, 4)),         # configs[3]: 4096^2 tiles (1024 spp in full)
     "c5": ("lights256", 2048, 2048, 64, 2, 8, "strong", (128, 16)),  # configs[4]: 256 emitters (512 spp in full)
 }
