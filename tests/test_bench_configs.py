@@ -1,0 +1,46 @@
+"""bench.py's workloads against BASELINE.json's configs (CPU only).
+
+Each bench config must render the resolution and bounce depth its BASELINE
+string names, and no more passes per step than the frame it is quoted on;
+c3's two default steps are exactly its 64-spp frame.
+"""
+import json
+import re
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402
+
+BASELINE = json.loads((ROOT / "BASELINE.json").read_text())["configs"]
+INDEX = {"c1": 0, "c2": 1, "c3": 2, "c4": 3, "c5": 4}
+
+
+def _parse(text):
+    w, h = map(int, re.search(r"(\d+)x(\d+)", text).groups())
+    spp = int(re.search(r"(\d+) spp", text).group(1))
+    m = re.search(r"(\d+) bounces", text)
+    return w, h, spp, int(m.group(1)) if m else None
+
+
+def test_every_baseline_config_has_a_bench_workload():
+    assert sorted(bench.CONFIGS) == sorted(INDEX)
+    assert len(BASELINE) == len(INDEX)
+
+
+def test_bench_workloads_match_baseline():
+    for name, i in INDEX.items():
+        scene, w, h, spp_step, steps, depth, scaling, _ = bench.CONFIGS[name]
+        bw, bh, bspp, bdepth = _parse(BASELINE[i])
+        assert (w, h) == (bw, bh), name
+        if bdepth is not None:
+            assert depth == bdepth, name
+        assert spp_step <= bspp and bspp % spp_step == 0, name
+        assert scaling in ("weak", "strong")
+
+
+def test_c3_default_run_is_the_whole_frame():
+    _, _, _, spp_step, steps, _, _, _ = bench.CONFIGS["c3"]
+    assert spp_step * steps == _parse(BASELINE[2])[2]
