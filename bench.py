@@ -313,15 +313,17 @@ def main():
         cnt = ctx.counters()
         state.copy_(sv)
         del sv
-        mine = [my_path_ms, cnt["paths"], cnt["traced_rays"]]
+        my_ops = roofline.ops_from_counters(cnt, n_spheres=len(desc.get("spheres", [])),
+                                            n_lights=len(desc.get("lights", [])))
+        mine = [my_path_ms, cnt["paths"], cnt["traced_rays"], my_ops]
         if dist:
-            # per-rank [path ms, paths, traced rays] as a [world, 3] all-reduce
-            # of one-hot rows (no list collectives needed)
-            allr = torch.zeros(world, 3, dtype=torch.float64)
+            # per-rank [path ms, paths, traced rays, op-eq] as a [world, 4]
+            # all-reduce of one-hot rows (no list collectives needed)
+            allr = torch.zeros(world, 4, dtype=torch.float64)
             allr[rank] = torch.tensor(mine, dtype=torch.float64)
             allr = host_coll(dist.all_reduce, allr)
             ranks = [{"rank": r, "path_ms": allr[r, 0].item(), "paths": int(allr[r, 1].item()),
-                      "traced_rays": int(allr[r, 2].item())} for r in range(world)]
+                      "traced_rays": int(allr[r, 2].item()), "ops": allr[r, 3].item()} for r in range(world)]
             ct = torch.tensor([cnt[k] for k in capi.COUNTER_NAMES], dtype=torch.int64)
             ct = host_coll(dist.all_reduce, ct)
             cnt = dict(zip(capi.COUNTER_NAMES, [int(x) for x in ct.tolist()]))
@@ -337,7 +339,7 @@ def main():
         paths_launch = total_paths // world // args.steps
         path_alg_bytes = roofline.path_bytes(paths_launch, cos_samples // world // args.steps,
                                              cnt["sphere_frames"] // world // args.steps)
-        traffic = traffic_src = occ = None
+        traffic = traffic_fabric = traffic_src = occ = dram = None
         for name in (f"pmc_latest_{args.config}.json",) + (("pmc_latest.json",) if args.config == "c2" else ()):
             pmc_file = ROOT / "profiles" / name
             if not pmc_file.exists():
@@ -347,11 +349,16 @@ def main():
                 c0 = pm.get("config", {})
                 if (c0.get("width") == W and c0.get("height") == H and c0.get("spp_per_step") == spp_step
                         and c0.get("depth_max", args.depth_max) == args.depth_max):
-                    traffic = pm.get("path_kernel_hbm_bytes_per_launch")
+                    # traffic: DRAM-destined bytes (TCC_EA0_RDREQ_DRAM / _WRREQ_DRAM share of
+                    # FETCH_SIZE / WRITE_SIZE); traffic_fabric: all L2 memory-side bytes
+                    traffic_fabric = pm.get("path_kernel_hbm_bytes_per_launch")
+                    dram = pm.get("path_kernel_dram")
+                    traffic = pm.get("path_kernel_dram_bytes_per_launch", traffic_fabric)
                     occ = pm.get("path_kernel_occupancy")
                     cfg_tag = f"_{pm['config_name']}" if pm.get("config_name") else ""
                     traffic_src = (f"profiles/{pm['tag']}{cfg_tag}_summary.json (rocprofv3 --pmc passes of the same "
-                                   f"config at N=1: FETCH_SIZE, WRITE_SIZE; SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE)")
+                                   f"config at N=1: FETCH_SIZE, WRITE_SIZE, TCC_EA0_RDREQ(_DRAM), "
+                                   f"TCC_EA0_WRREQ(_DRAM); SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE)")
                     break
             except Exception:
                 traffic = occ = None
@@ -368,8 +375,12 @@ def main():
             "frac": hbm_ach / roofline.HBM_PEAK_GBPS,
             "traffic": traffic,
             "traffic_unit": "bytes/launch",
+            "traffic_kind": ("dram" if dram else "fabric") if traffic else None,
+            "traffic_fabric": traffic_fabric,
+            "traffic_dram_detail": dram,
             "traffic_source": traffic_src,
             "measured_GBps": (traffic / launch_s / 1e9) if traffic else None,
+            "measured_fabric_GBps": (traffic_fabric / launch_s / 1e9) if traffic_fabric else None,
             "kernel": "raygen_kernel + path_kernel",
             "bytes_per_path": path_alg_bytes / paths_launch,
             "compulsory": {
@@ -468,6 +479,10 @@ def main():
             if ranks:
                 pm = [r["path_ms"] for r in ranks]
                 out["rank_imbalance"] = max(pm) / (sum(pm) / len(pm))
+                # the work each rank did (algorithmic op-eq from its event
+                # counters), independent of timing: max / mean over ranks
+                wk = [r["ops"] for r in ranks]
+                out["work_imbalance"] = max(wk) / (sum(wk) / len(wk))
             out["frame_end"] = (f"one gather of the owned rows to rank 0: {tiles.payload_bytes(W, owned_rows)} B "
                                 f"({16 * W * max_own} B per rank, 16 B per owned pixel)")
             if verify is not None:

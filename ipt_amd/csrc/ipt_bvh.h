@@ -40,6 +40,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <vector>
 
@@ -208,16 +210,32 @@ inline void bvh_build_spheres(const float* cr, int n, const float cam[3], float 
 // (3D DDA) and stops once the next cell starts beyond the best hit, so a walk
 // costs the cells along the (short) ray instead of a root-to-leaf descent per
 // candidate. Exactness, with the BVH's padded sphere boxes and margin:
-// * every padded box (ipt_bvh.h header) is registered, inflated by m, in every
-//   cell it overlaps (ranges computed in double, rounded outward);
-// * the DDA's float rounding (approximate reciprocals, cell-boundary t's) can
-//   only make it visit a cell adjacent to the exact ray's where the ray passes
-//   within ~1e-6 |t| of a cell edge — far inside m = 1e-4 (1 + max |coord|),
-//   so every padded box the exact ray meets is registered in a visited cell;
+// * registration: a sphere's padded box (ipt_bvh.h header) is the bound of
+//   its padded ball (centre c, radius R = r + pad: the box's half-width), and
+//   any ray the exact sphere_t accepts passes within R of c. With
+//   IPT_GRID_SPHERE_REG (default) the sphere is registered in every cell of
+//   its box range (inflated by m, computed in double, rounded outward) whose
+//   distance to the box centre is at most R + m + 1e-6 (1 + |c|_1) (the last
+//   term covers the box centre's offset from the float centre, i.e. the
+//   roundings of c -+ r), times (1 + 1e-9); without it, in every cell of the
+//   box range;
+// * walk: the DDA's float rounding (approximate reciprocals, cell-boundary
+//   t's) can only make it visit a cell adjacent to the exact ray's where the
+//   ray passes within ~1e-6 |t| of a cell edge. Let q be the exact ray's
+//   point nearest c, inside the ball, and Q the cell holding q: Q is within
+//   R of c, hence registered; where the DDA strays it visits instead a
+//   neighbour of Q whose distance to q is < 1e-6 |t|, far inside m = 1e-4
+//   (1 + max |coord|), so that neighbour is within R + m of c and registered
+//   too. Every accepted sphere is therefore in a cell the walk visits at
+//   some t <= (ball entry t) + m, and the ball's entry t is >= the padded
+//   box's entry t;
 // * it stops after a cell whose exit t exceeds (best*1.0001 + 1e-5 + tmargin
 //   + m) * (1 + 1e-5) + 1e-5: a sphere registered only in later cells has its
-//   padded box entry beyond that, and (tmargin: tangency t-error) cannot
-//   produce a computed t below or equal to best;
+//   ball entry (>= its box entry) beyond best + tmargin, and (tmargin:
+//   tangency t-error) cannot produce a computed t below or equal to best;
+// * order: each cell's items are in ascending original index (the fill loop
+//   runs over i in order; checked after the fill), which the wave walk's
+//   (t bits, item position) slot key relies on for the lowest-index tie rule;
 // * ties: equal t is broken by the lowest original index, as in the BVH
 //   (spheres registered in several cells are tested again, harmlessly).
 struct SphereGrid {
@@ -360,6 +378,14 @@ inline bool grid_build_spheres(const float* cr, int n, const float cam[3], float
                     }
         }
     }
+    // the wave walk's tie rule needs every cell in ascending index order: an
+    // internal invariant, so a violation (a changed fill order) aborts loudly
+    for (size_t c = 0; c < cells; ++c)
+        for (int k = g.start[c] + 1; k < g.start[c + 1]; ++k)
+            if (!(g.items[k - 1].index < g.items[k].index)) {
+                std::fprintf(stderr, "ipt: sphere grid cell %zu not in ascending index order\n", c);
+                std::abort();
+            }
     return true;
 }
 

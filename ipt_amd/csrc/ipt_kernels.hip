@@ -564,7 +564,7 @@ template <bool COUNT>
 __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool walking, vec3 o, vec3 d, int& cell,
                                                       vec3& tmx, float& best, int& bidx, int budget,
                                                       unsigned long long* slots, uint8_t* own, int lane,
-                                                      uint32_t& c_nodes, uint32_t& c_tests) {
+                                                      uint32_t& c_nodes, uint32_t& c_tests IPT_DIAG_PARAMS) {
     const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     auto lin_of = [&](int c) {
         return (c & 0xff) + kp.grid_n[0] * (((c >> 8) & 0xff) + kp.grid_n[1] * (c >> 16));
@@ -581,6 +581,14 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
         // IPT_GRID_WAVE_FLOOR lanes walk; they resume in the next step)
         const uint64_t am = __ballot(act);
         if (!am || (it >= IPT_GRID_WAVE_FLOOR_IT && __popcll(am) < IPT_GRID_WAVE_FLOOR)) break;
+#if IPT_PROF
+        // phase 6 (walk cell): one wave iteration, its walking lanes (every
+        // lane of the wave runs this loop, so lane 0 counts)
+        if (prof_w && lane == 0) {
+            prof_w[6] += 1u;
+            prof_l[6] += (uint32_t)__popcll(am);
+        }
+#endif
         // the next cell (from tmx alone) and its range, in flight during the tests
         int ncell = 0, n0 = 0, n1 = 0;
         vec3 ntm = tmx;
@@ -2053,7 +2061,8 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                                                   wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes, c_tests);
                 else
                     sphere_grid_walk_wave<COUNT>(kg, tracing, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
-                                                 wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes, c_tests);
+                                                 wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes,
+                                                 c_tests IPT_DIAG_ARGS);
             }
             if (tracing && xi < 0) {
                 tracing = false;
@@ -2531,6 +2540,7 @@ struct ipt_ctx {
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
     int blocks_per_cu = 0;      // of the last path-kernel launch
     bool lattice_lds = true;    // IPT_LATTICE_LDS=0: the lattice instances with global records (tests)
+    size_t max_lds = 160 * 1024;  // the device's LDS per workgroup (hipDeviceAttributeMaxSharedMemoryPerBlock)
 };
 
 namespace {
@@ -2668,7 +2678,11 @@ int validate(ipt_ctx* ctx, const ipt_params* p) {
     if ((int64_t)p->width * p->height > (int64_t)1 << 31)
         return fail(ctx, IPT_E_INVALID, "frame larger than 2^31 pixels");
     if (p->spp < 0 || p->spp_offset < 0) return fail(ctx, IPT_E_INVALID, "negative spp");
-    if (p->n_rays < 0 || p->n_rays > 64) return fail(ctx, IPT_E_UNSUPPORTED, "n_rays must be in [0,64]");
+    // a suspended level stores its iteration count in the 8 low bits of its
+    // meta word (ti | kind << 8, ti <= n_rays), and n_rays < 256 bounds the
+    // pushed depth by 7 (a node at depth d has n_rays >> d children), so every
+    // depth_max fits the MAXSUSP = 8 instances
+    if (p->n_rays < 0 || p->n_rays > 255) return fail(ctx, IPT_E_UNSUPPORTED, "n_rays must be in [0,255]");
     if (p->depth_max < 0 || p->depth_max > 64) return fail(ctx, IPT_E_INVALID, "depth_max out of range");
     if (p->n_shards > 1 && (p->shard_id < 0 || p->shard_id >= p->n_shards))
         return fail(ctx, IPT_E_INVALID, "shard_id out of range");
@@ -2696,7 +2710,6 @@ size_t path_lds_bytes(const KParams& kp) {
                                 : 0)) *
            sizeof(float);
 }
-constexpr size_t kMaxLdsBytes = 160 * 1024;  // per workgroup (and per CU) on gfx950
 
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
@@ -2749,12 +2762,12 @@ int launch_path2(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
         // the records-in-LDS instance wherever its LDS fits one workgroup per CU
         constexpr int G = IPT_GEOM_SPHERE_IN_BOX;
         if (ctx->lgrid.pattern == 1 && kp.geometry_kind == G) {
-            if (IPT_LAX_LDS && ctx->lattice_lds && path_lds_bytes<MAXSUSP, kLightsGridA10L, G>(kp) <= kMaxLdsBytes)
+            if (IPT_LAX_LDS && ctx->lattice_lds && path_lds_bytes<MAXSUSP, kLightsGridA10L, G>(kp) <= ctx->max_lds)
                 return launch_path4<MAXSUSP, COUNT, kLightsGridA10L, G>(ctx, kp, st);
             return launch_path4<MAXSUSP, COUNT, kLightsGridA10, G>(ctx, kp, st);
         }
         if (ctx->lgrid.pattern == 2 && kp.geometry_kind == G) {
-            if (IPT_LAX_LDS && ctx->lattice_lds && path_lds_bytes<MAXSUSP, kLightsGridA01L, G>(kp) <= kMaxLdsBytes)
+            if (IPT_LAX_LDS && ctx->lattice_lds && path_lds_bytes<MAXSUSP, kLightsGridA01L, G>(kp) <= ctx->max_lds)
                 return launch_path4<MAXSUSP, COUNT, kLightsGridA01L, G>(ctx, kp, st);
             return launch_path4<MAXSUSP, COUNT, kLightsGridA01, G>(ctx, kp, st);
         }
@@ -2985,6 +2998,16 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     ipt_ctx* ctx = new ipt_ctx();
     ctx->device = hip_device;
     ctx->n_cu = prop.multiProcessorCount;
+    {
+        // the records-in-LDS lattice instances are chosen against the device's
+        // own limit (160 KiB on gfx950), so a smaller one falls back to the
+        // global-record instances instead of failing the launch
+        // (the larger of the per-block limit and its opt-in value)
+        int lds = 0, optin = 0;
+        if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) != hipSuccess) lds = 0;
+        if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, hip_device) != hipSuccess) optin = 0;
+        if (std::max(lds, optin) > 0) ctx->max_lds = (size_t)std::max(lds, optin);
+    }
     if (const char* e = std::getenv("IPT_BLOCKS_PER_CU")) ctx->bpc_override = std::atoi(e);  // profiling only
     if (const char* e = std::getenv("IPT_LNODES_LDS")) ctx->lnodes_lds = std::atoi(e) != 0;
     if (const char* e = std::getenv("IPT_LIGHT_GRID")) ctx->light_grid_on = std::atoi(e) != 0;

@@ -105,6 +105,8 @@
 #ifndef IPT_GRID_WAVE_FLOOR_IT
 #define IPT_GRID_WAVE_FLOOR_IT 0  // ... but not before this many cell iterations
 #endif
+// the two-cell wave walk reads the packed items and their separate index array
+static_assert(IPT_GRID_WAVE != 2 || IPT_GRID_C4, "IPT_GRID_WAVE=2 needs IPT_GRID_C4 (kp.grid_c4 / grid_idx)");
 
 // ---- walk budgets and acceleration-structure parameters
 #ifndef IPT_GRID_INLINE

@@ -229,30 +229,6 @@ IPT_HD float sphere_t(float radius, vec3 o, vec3 d) {
     return t;
 }
 
-// intersection_with_sphere in two parts for the sphere lists' walks: the
-// discriminant (its `desc < 0` rejection is the common outcome), and the rest
-// of the test for a desc that passed. sphere_t<false, false>(r, o, d) ==
-// (sphere_desc(r, o, d, &b) < 0 ? inf : sphere_tail(b, desc, o, d)): the same
-// operations in the same order.
-IPT_HD float sphere_desc(float radius, vec3 o, vec3 d, float* b_out) {
-    const float b = dot(o, d);
-    *b_out = b;
-    return 4.0f * (b * b) - 4.0f * (dot(o, o) - radius * radius);
-}
-IPT_HD float sphere_tail(float b, float desc, vec3 o, vec3 d) {
-    const float sd = sqrt_(desc);
-    const float m2b = -2.0f * b;
-    float t1 = (m2b - sd) * 0.5f;
-    float t2 = (m2b + sd) * 0.5f;
-    if (lt_1em6(t1)) t1 = inf_();
-    if (lt_1em6(t2)) t2 = inf_();
-    const float t = (t2 < t1) ? t2 : t1;  // std::min(t1, t2)
-    if (t == inf_()) return t;
-    const vec3 pos = o + d * t;
-    if (dot(pos, o - pos) <= 0.0f) return inf_();
-    return t;
-}
-
 // The facing plane of axis a (sgn chosen so that sgn*d_a > 0 unless d_a is a
 // zero): dp = sgn*d_a equals |d_a| whenever |dp| >= 1e-6 (otherwise the test
 // misses either way), so `dp < 0` never decides, and 1 - sgn*o_a is one

@@ -8,8 +8,10 @@ T=${TAG:-latest}
 for c in ${CFGS:-c2 c3 c5}; do
   B="python3 bench.py --config $c --steps 2 --warmup 1 --cpu-seconds 0 --no-counters"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_${c}_stats -o run -- $B > gpurun_out/${T}_${c}_stats.json 2> gpurun_out/${T}_${c}_stats.err || { echo "$c stats failed"; tail gpurun_out/${T}_${c}_stats.err; exit 1; }
-  for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
-    n=$(echo $pass | cut -d' ' -f1)
+  for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+              "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_32B_sum GRBM_GUI_ACTIVE" \
+              "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"; do
+    n=$(echo $pass | cut -d' ' -f1-2 | tr ' ' '+')
     timeout -s KILL 300 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d gpurun_out/${T}_${c}_pmc_$n -o run -- $B > gpurun_out/${T}_${c}_pmc_$n.json 2> gpurun_out/${T}_${c}_pmc_$n.err || { echo "$c pmc $n failed"; tail gpurun_out/${T}_${c}_pmc_$n.err; exit 1; }
   done
   python3 scripts/summarize_rocprof.py $T $c gpurun_out/${T}_${c}_stats.json gpurun_out/${T}_${c}_stats gpurun_out/${T}_${c}_pmc_* || exit 1

@@ -75,6 +75,26 @@ if "FETCH_SIZE" in pk and "WRITE_SIZE" in pk:
     b = (pk["FETCH_SIZE"] + pk["WRITE_SIZE"]) * 1024
     summary["path_kernel_hbm_bytes_per_launch"] = b
     summary["path_kernel_hbm_bytes_per_path"] = b / paths_per_launch
+# DRAM share of the fabric traffic (TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ: the
+# L2's memory-side read requests "destined for DRAM (MC)"; likewise writes).
+# The Infinity Cache sits on the memory side of that interface, so its hits
+# may still be counted as DRAM-destined: an upper bound on HBM bytes.
+if "TCC_EA0_RDREQ_sum" in pk and "TCC_EA0_RDREQ_DRAM_sum" in pk and "FETCH_SIZE" in pk:
+    rd_share = pk["TCC_EA0_RDREQ_DRAM_sum"] / max(pk["TCC_EA0_RDREQ_sum"], 1.0)
+    wr_share = 1.0
+    if "TCC_EA0_WRREQ_sum" in pk and "TCC_EA0_WRREQ_DRAM_sum" in pk:
+        wr_share = pk["TCC_EA0_WRREQ_DRAM_sum"] / max(pk["TCC_EA0_WRREQ_sum"], 1.0)
+    dram = (pk["FETCH_SIZE"] * rd_share + pk.get("WRITE_SIZE", 0.0) * wr_share) * 1024
+    summary["path_kernel_dram_bytes_per_launch"] = dram
+    summary["path_kernel_dram_bytes_per_path"] = dram / paths_per_launch
+    summary["path_kernel_dram"] = {
+        "read_requests": pk["TCC_EA0_RDREQ_sum"], "read_requests_dram": pk["TCC_EA0_RDREQ_DRAM_sum"],
+        "read_dram_share": rd_share, "write_dram_share": wr_share,
+        "read_requests_32B": pk.get("TCC_EA0_RDREQ_32B_sum"),
+        "dram_credit_stall_cycles": pk.get("TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"),
+        "source": ("(FETCH_SIZE x RDREQ_DRAM/RDREQ + WRITE_SIZE x WRREQ_DRAM/WRREQ) x 1024; the Infinity "
+                   "Cache is memory-side, so DRAM-destined requests may include its hits (upper bound)"),
+    }
 if "SQ_WAVE_CYCLES" in pk and "GRBM_GUI_ACTIVE" in pk:
     busy = pk["GRBM_GUI_ACTIVE"] / N_XCD  # GPU-busy cycles of the dispatch
     summary["path_kernel_occupancy"] = {
@@ -88,7 +108,8 @@ if "SQ_WAVE_CYCLES" in pk and "GRBM_GUI_ACTIVE" in pk:
         t = sum(durations["path_kernel"]) / len(durations["path_kernel"])
         summary["path_kernel_occupancy"]["effective_clock_GHz"] = busy / t / 1e9
 for key in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
-            "TCC_HIT_sum", "TCC_MISS_sum"):
+            "TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum",
+            "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"):
     if key in pk:
         summary.setdefault("path_kernel_per_path", {})[key] = pk[key] / paths_per_launch
 ak = pmc.get("accumulate_kernel", {})
@@ -97,4 +118,5 @@ if "FETCH_SIZE" in ak and "WRITE_SIZE" in ak:
 json.dump(summary, open(out / f"{tag}_{cfg_name}_summary.json", "w"), indent=1)
 json.dump(summary, open(out / f"pmc_latest_{cfg_name}.json", "w"), indent=1)
 print(json.dumps({k: summary.get(k) for k in ("tag", "config_name", "path_kernel_hbm_bytes_per_path",
+                                              "path_kernel_dram_bytes_per_path",
                                               "path_kernel_occupancy", "path_kernel_per_path")}, indent=1))
