@@ -82,6 +82,9 @@ def parse():
                     help="CPU-baseline threads (0 = this process's CPU share, see cpu_threads())")
     ap.add_argument("--no-counters", action="store_true",
                     help="skip the (untimed) counting re-render used for the roofline")
+    ap.add_argument("--sync", action="store_true",
+                    help="one synchronous ipt_render_device per step instead of queuing the steps with "
+                         "ipt_render_device_async (which lets each step's launch fill the previous one's tail)")
     ap.add_argument("--verify", action="store_true",
                     help="N>1: rank 0 re-renders the whole frame unsharded after the timing and "
                          "compares it bit for bit with the assembled one")
@@ -133,6 +136,19 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def physical_cores() -> int | None:
+    """Physical cores of the host (distinct (package, core) pairs in sysfs)."""
+    import glob
+
+    ids = set()
+    for d in glob.glob("/sys/devices/system/cpu/cpu[0-9]*/topology"):
+        try:
+            ids.add((open(f"{d}/physical_package_id").read().strip(), open(f"{d}/core_id").read().strip()))
+        except OSError:
+            pass
+    return len(ids) or None
+
+
 def cpu_baseline(args, desc):
     """The oracle (oracle/ipt_oracle.cpp, the recursive CPU restatement of the
     reference estimator with glibc libm) timed on this host's cores over a
@@ -166,6 +182,22 @@ def cpu_baseline(args, desc):
         rs, cs = args.cpu_sample
         nr, nc = (H + rs - 1) // rs, (W + cs - 1) // cs
         vals = np.zeros(nr * nc, np.float32)
+        # the same sample on ONE thread for a bounded time first: the per-core
+        # rate the multi-thread figure is scaled against (the job's 16-CPU
+        # share is the most this box allows: a full-host run is not measured,
+        # it is extrapolated from the per-core rate below)
+        one_total, one_calls, t1 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t1 < min(8.0, args.cpu_seconds / 3):
+            p = capi.make_params(W, H, 1, spp_offset=10_000 + one_calls, n_rays=args.n_rays,
+                                 depth_max=args.depth_max, seed=args.seed)
+            rp, cp = (37 * one_calls) % rs, (11 * one_calls) % cs
+            rc = lib.ipt_oracle_render_rows_values(C.addressof(s), C.addressof(p), rs, rp, cs, cp, 1,
+                                                   vals.ctypes.data)
+            assert rc == 0
+            one_total += len(range(rp, H, rs)) * len(range(cp, W, cs))
+            one_calls += 1
+        one_rate = one_total / (time.perf_counter() - t1)
+        t0 = time.perf_counter()
         while True:
             # call k: rows (37k mod rs) (mod rs), columns (11k mod cs) (mod cs)
             # of pass k: co-prime strides walk every row and column phase
@@ -182,7 +214,8 @@ def cpu_baseline(args, desc):
                 break
         sample = (f"{calls} calls, each the source pixels at row stride {rs} and column stride {cs} of one "
                   f"pass (phases 37k mod {rs}, 11k mod {cs}) of the {W}x{H} frame: {total} paths in {el:.1f} s")
-    return {
+    phys = physical_cores()
+    out = {
         "value": total / el / 1e6,
         "unit": "Mpaths/s",
         "cores": threads,
@@ -193,7 +226,19 @@ def cpu_baseline(args, desc):
         "cpu_model": cpu_model(),
         "host_cpus": os.cpu_count(),
         "paths_per_s_per_core": total / el / threads,
+        "host_physical_cores": phys,
+        "threads_policy": ("the job's CPU share (OMP_NUM_THREADS, 16 per GPU on the GPU box): the pool allows no "
+                           "more threads per job; a full-host figure is extrapolated, not measured"),
     }
+    if args.cpu_sample is not None:
+        out["single_thread_paths_per_s"] = one_rate
+        out["thread_scaling"] = (total / el) / one_rate if one_rate > 0 else None
+        if phys:
+            out["full_host_extrapolated_Mpaths_s"] = one_rate * phys / 1e6
+            out["full_host_note"] = (f"single-thread rate x {phys} physical cores (linear scaling assumed; "
+                                     f"measured scaling at {threads} threads: "
+                                     f"{(total / el) / one_rate / threads:.2f} of linear)")
+    return out
 
 
 def main():
@@ -244,6 +289,18 @@ def main():
     def render(p, st=state):
         ctx.render_device(p, st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(), st[3].data_ptr(), stream)
 
+    # the steps are queued (ipt_render_device_async: a step's path kernel takes
+    # the CUs the previous step's tail leaves idle; the GridRenderPlane replays
+    # stay in step order on `stream`) and waited for once
+    use_async = ctx.has_async and not args.sync
+
+    def render_step(p):
+        if use_async:
+            ctx.render_device_async(p, state[0].data_ptr(), state[1].data_ptr(), state[2].data_ptr(),
+                                    state[3].data_ptr(), stream)
+        else:
+            render(p)
+
     # the tile plan of every rank (host-only, deterministic): owned rows
     owned_rows = tiles.owned_rows(W, H, args.tile_rows, world)
     max_own = max(len(o) for o in owned_rows)
@@ -259,7 +316,9 @@ def main():
 
     # warmup (separate passes, then reset the image)
     for i in range(args.warmup):
-        render(params(spp_step, 1_000_000 + i * spp_step))
+        render_step(params(spp_step, 1_000_000 + i * spp_step))
+    if use_async:
+        ctx.wait()
     state.zero_()
     torch.cuda.synchronize(dev)
 
@@ -269,10 +328,14 @@ def main():
     t0 = time.perf_counter()
     path_ms = acc_ms = 0.0
     for step in range(args.steps):
-        render(params(spp_step, step * spp_step))
-        pm, am = ctx.last_kernel_ms()
-        path_ms += pm
-        acc_ms += am
+        render_step(params(spp_step, step * spp_step))
+        if not use_async:
+            pm, am = ctx.last_kernel_ms()
+            path_ms += pm
+            acc_ms += am
+    if use_async:
+        ctx.wait()
+        path_ms, acc_ms = ctx.last_kernel_ms()  # all the steps' launches (overlaps counted once)
     if dist:
         tiles.assemble(dist, state, owned_rows, rank, host=share)
     torch.cuda.synchronize(dev)
@@ -461,6 +524,8 @@ def main():
                        "width": W, "height": H, "spp": spp_total,
                        "spp_per_step": spp_step, "depth_max": args.depth_max,
                        "n_rays": args.n_rays, "tile_rows": args.tile_rows if world > 1 else 0,
+                       "calls": ("queued (ipt_render_device_async), one wait" if use_async
+                                 else "synchronous ipt_render_device per step"),
                        "parallelism": f"tiles{world}",
                        "per_rank": ("the whole frame's tiles dealt round-robin; " +
                                     (f"{args.spp_per_step} x N passes per step (weak)" if weak

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IPT_ABI_VERSION 3
+#define IPT_ABI_VERSION 4
 
 enum {
     IPT_OK = 0,
@@ -198,12 +198,27 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* scene);
 /* Host buffers: copies the image in, renders p->spp passes, copies it out. */
 int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* host_img);
 
-/* Device buffers (hipMalloc'd or torch CUDA tensors), kernels launched on
-   `hip_stream` (NULL = the context's own stream) after the work already queued
-   there. Synchronous: the call returns when the image is complete (it waits
-   for the path and accumulate kernels of every chunk; ipt_last_kernel_ms then
-   holds their times). */
+/* Device buffers (hipMalloc'd or torch CUDA tensors). The GridRenderPlane
+   replays run on `hip_stream` (NULL = the context's own stream) after the work
+   already queued there, in call order; the per-sample work (raygen + path
+   kernel) runs on the context's two work-slot streams, consecutive launches
+   alternating, so a launch fills the CUs its predecessor's tail leaves idle.
+   Synchronous: the call returns when the image is complete (it waits for the
+   path and accumulate kernels of every chunk and of every call queued before
+   it; ipt_last_kernel_ms then holds their times). */
 int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, void* hip_stream);
+
+/* The same, returning once the launches are queued (the progressive loop of
+   main.cpp:256-285 without a host wait per pass): the image is complete when
+   `hip_stream` reaches the point after the call, or after ipt_render_wait.
+   The image buffers must stay valid until then. Calls into the same image on
+   the same stream accumulate exactly as sequential synchronous calls
+   (bit-identical). ipt_upload_scene, the counter calls and ipt_destroy wait
+   for queued work first. */
+int ipt_render_device_async(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, void* hip_stream);
+/* Waits for every queued render; ipt_last_kernel_ms then holds the times of
+   the launches since the previous wait (a synchronous render call waits). */
+int ipt_render_wait(ipt_ctx* ctx);
 
 /* Per-sample radiance, for bit-exact verification: values[s][iy][ix] is the
    clamped root ray_power of pass p->spp_offset+s at source pixel (ix,iy)
@@ -227,9 +242,12 @@ int ipt_reset_counters(ipt_ctx* ctx);
  * Cleared by ipt_reset_counters. */
 int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n);
 
-/* Timing of the most recent render call's kernels (ms, HIP events on the
-   launch stream, summed over its chunks): [0] = the path's per-sample work,
-   raygen_kernel + path_kernel (raygen ~0.2 % of it); [1] = accumulate kernel. */
+/* Timing of the kernels of the render calls completed by the most recent wait
+   (a synchronous render, or ipt_render_wait after asynchronous ones): ms from
+   HIP events, summed over their launches: [0] = the path's per-sample work,
+   raygen_kernel + path_kernel (raygen ~0.2 % of it), each launch counted from
+   its start or from its predecessor's end, whichever is later (overlapped
+   launches sum to their span); [1] = accumulate kernels. */
 int ipt_last_kernel_ms(ipt_ctx* ctx, float* path_ms, float* accumulate_ms);
 
 /* ---- image post-process on the GPU, bit-exact --------

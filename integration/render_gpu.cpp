@@ -2,83 +2,206 @@
 // maintainer adds to dimalit/ipt to render sample passes through
 // libipt_hip.so instead of calling render_sample (src/main.cpp:186-223) per
 // pass. It is compiled against the reference's own headers
-// (oracle/build_ref.sh, tests/test_reference_adapter.py), with the one
-// change the reference needs: AreaLight keeps x_axis / y_axis / type private
-// (src/lighting/lighting.h:20-23), so the maintainer adds, in its public
-// section,
-//     glm::vec3 xAxis() const { return x_axis; }
-//     glm::vec3 yAxis() const { return y_axis; }
-//     type_t lightType() const { return type; }
+// (oracle/build_ref.sh, tests/test_reference_adapter.py), with the accessors
+// the reference needs for fields it keeps private, added by the maintainer
+// in the public sections:
+//   AreaLight (src/lighting/lighting.h:20-23)
+//       glm::vec3 xAxis() const { return x_axis; }
+//       glm::vec3 yAxis() const { return y_axis; }
+//       type_t lightType() const { return type; }
+//   FractalSpheres (src/geometry/FractalSpheres.h:13-14)
+//       const std::vector<float>& radii() const { return rs; }
+//       const std::vector<glm::vec3>& centers() const { return cs; }
+// Every sample_scenes entry (src/sample_scenes.cpp:20-108) flattens: the
+// geometries GeometrySphereInBox, GeometryFloor, GeometryCorner,
+// FractalSpheres and GeometrySmallPt, and CollectionLighting's AreaLight
+// (square and triangle), SphereLight, PointLight and InvertedSphereLight
+// (addOuterLight). Anything else throws.
 #include "ipt_capi.h"  // include/ipt_capi.h from this repo
 
 #include <CollectionLighting.h>
 #include <GridRenderPlane.h>
 #include <SimpleCamera.h>
+#include <geometry/FractalSpheres.h>
+#include <geometry/GeometryCorner.h>
+#include <geometry/GeometryFloor.h>
+#include <geometry/GeometrySmallPt.h>
 #include <geometry/GeometrySphereInBox.h>
 #include <lighting/lighting.h>
 
 #include <algorithm>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <vector>
 
-// Scene (tracer_interfaces.h:45-49) -> ipt_scene; sample_scenes[0]'s classes
-// (GeometrySphereInBox, CollectionLighting of AreaLights, SimpleCamera).
-static ipt_scene flatten(const Scene& s, std::vector<ipt_area_light>& lights) {
-    ipt_scene out{};
-    if (!std::dynamic_pointer_cast<const GeometrySphereInBox>(s.geometry))
+namespace {
+
+// The flattened scene and the arrays it points into.
+struct Flat {
+    ipt_scene sc{};
+    std::vector<ipt_area_light> lights;
+    std::vector<ipt_sphere> spheres;
+    bool operator==(const Flat& o) const {
+        auto same = [](const void* a, const void* b, size_t n) { return n == 0 || std::memcmp(a, b, n) == 0; };
+        return sc.geometry_kind == o.sc.geometry_kind && lights.size() == o.lights.size() &&
+               spheres.size() == o.spheres.size() &&
+               same(&sc.camera, &o.sc.camera, sizeof(ipt_camera)) &&
+               same(lights.data(), o.lights.data(), lights.size() * sizeof(ipt_area_light)) &&
+               same(spheres.data(), o.spheres.data(), spheres.size() * sizeof(ipt_sphere));
+    }
+};
+
+void put3(float* d, const glm::vec3& v) {
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+}
+
+// GeometrySmallPt's room: the `spheres[]` table is local to its translation
+// unit (src/geometry/GeometrySmallPt.cpp:23-32), so the adapter restates its
+// radii and positions (the vec3 constructor's float roundings); the library
+// intersects them in double as Sphere::intersect does.
+void smallpt_spheres(std::vector<ipt_sphere>& out) {
+    const struct {
+        double rad;
+        glm::vec3 p;
+    } room[] = {{1e3, glm::vec3(1e3 + 1, 40.8, 81.6)},  {1e3, glm::vec3(-1e3 + 99, 40.8, 81.6)},
+                {1e3, glm::vec3(50, 40.8, 1e3)},         {1e3, glm::vec3(50, 1e3, 81.6)},
+                {1e3, glm::vec3(50, -1e3 + 81.6, 81.6)}, {16.5, glm::vec3(27, 16.5, 47)},
+                {16.5, glm::vec3(73, 16.5, 78)}};
+    for (const auto& s : room) {
+        ipt_sphere q{};
+        put3(q.center, s.p);
+        q.radius = (float)s.rad;  // 1e3 and 16.5 are exact in float
+        out.push_back(q);
+    }
+}
+
+// Scene (tracer_interfaces.h:45-49) -> ipt_scene
+void flatten(const Scene& s, Flat& f) {
+    f = Flat{};
+    if (std::dynamic_pointer_cast<const GeometrySphereInBox>(s.geometry)) {
+        f.sc.geometry_kind = IPT_GEOM_SPHERE_IN_BOX;
+    } else if (std::dynamic_pointer_cast<const GeometryFloor>(s.geometry)) {
+        f.sc.geometry_kind = IPT_GEOM_FLOOR;
+    } else if (std::dynamic_pointer_cast<const GeometryCorner>(s.geometry)) {
+        f.sc.geometry_kind = IPT_GEOM_CORNER;
+    } else if (auto fr = std::dynamic_pointer_cast<const FractalSpheres>(s.geometry)) {
+        f.sc.geometry_kind = IPT_GEOM_SPHERES;
+        const auto& rs = fr->radii();
+        const auto& cs = fr->centers();
+        for (size_t i = 0; i < rs.size(); ++i) {
+            ipt_sphere q{};
+            put3(q.center, cs[i]);
+            q.radius = rs[i];
+            f.spheres.push_back(q);
+        }
+    } else if (std::dynamic_pointer_cast<const GeometrySmallPt>(s.geometry)) {
+        f.sc.geometry_kind = IPT_GEOM_SMALLPT;
+        smallpt_spheres(f.spheres);
+    } else {
         throw std::runtime_error("geometry not supported by libipt_hip");
-    out.geometry_kind = IPT_GEOM_SPHERE_IN_BOX;
+    }
     auto coll = std::dynamic_pointer_cast<const CollectionLighting>(s.lighting);
     if (!coll) throw std::runtime_error("lighting must be a CollectionLighting");
     for (auto& l : coll->lights) {
-        auto a = std::dynamic_pointer_cast<const AreaLight>(l);
-        if (!a) throw std::runtime_error("only AreaLight is supported");
         ipt_area_light L{};
-        const glm::vec3 x = a->xAxis(), y = a->yAxis();
-        for (int k = 0; k < 3; ++k) {
-            L.position[k] = a->position[k];
-            L.x_axis[k] = x[k];
-            L.y_axis[k] = y[k];
+        L.power = l->power;
+        put3(L.position, l->position);
+        if (auto a = std::dynamic_pointer_cast<const AreaLight>(l)) {
+            put3(L.x_axis, a->xAxis());
+            put3(L.y_axis, a->yAxis());
+            L.type = a->lightType() == AreaLight::TYPE_TRIANLE ? IPT_LIGHT_AREA_TRIANGLE : IPT_LIGHT_AREA_DIAMOND;
+        } else if (auto o = std::dynamic_pointer_cast<const InvertedSphereLight>(l)) {  // before SphereLight
+            L.x_axis[0] = o->radius;
+            L.type = IPT_LIGHT_OUTER_SPHERE;
+        } else if (auto sl = std::dynamic_pointer_cast<const SphereLight>(l)) {
+            L.x_axis[0] = sl->radius;
+            L.type = IPT_LIGHT_SPHERE;
+        } else if (std::dynamic_pointer_cast<const PointLight>(l)) {
+            L.type = IPT_LIGHT_POINT;  // its virtual radius is not stored (lighting.h:31-42)
+        } else {
+            throw std::runtime_error("light type not supported by libipt_hip");
         }
-        L.power = a->power;
-        L.type = a->lightType() == AreaLight::TYPE_TRIANLE ? IPT_LIGHT_AREA_TRIANGLE : IPT_LIGHT_AREA_DIAMOND;
-        lights.push_back(L);
+        f.lights.push_back(L);
     }
-    out.n_lights = (int)lights.size();
-    out.lights = lights.data();
     auto cam = std::dynamic_pointer_cast<const SimpleCamera>(s.camera);
     if (!cam) throw std::runtime_error("camera must be a SimpleCamera");
-    for (int k = 0; k < 3; ++k) {
-        out.camera.position[k] = cam->position[k];
-        out.camera.direction[k] = cam->direction[k];
-        out.camera.right[k] = cam->right[k];
-        out.camera.up[k] = cam->up[k];
-    }
-    return out;
+    put3(f.sc.camera.position, cam->position);
+    put3(f.sc.camera.direction, cam->direction);
+    put3(f.sc.camera.right, cam->right);
+    put3(f.sc.camera.up, cam->up);
+    f.sc.n_lights = (int)f.lights.size();
+    f.sc.lights = f.lights.data();
+    f.sc.n_spheres = (int)f.spheres.size();
+    f.sc.spheres = f.spheres.empty() ? nullptr : f.spheres.data();
 }
 
-// spp passes of render_sample into `plane`, continuing its running means
-// (GridRenderPlane::addRay semantics, bit-exact against the CPU restatement)
+}  // namespace
+
+// One context on one device; the scene is uploaded again only when its
+// flattened content changes (a progressive loop renders one scene many times).
+class GpuRenderer {
+public:
+    explicit GpuRenderer(int device = 0) {
+        if (ipt_create(device, &ctx_) != IPT_OK) throw std::runtime_error(ipt_last_error(nullptr));
+    }
+    ~GpuRenderer() { ipt_destroy(ctx_); }
+    GpuRenderer(const GpuRenderer&) = delete;
+    GpuRenderer& operator=(const GpuRenderer&) = delete;
+
+    // spp passes of render_sample into `plane`, continuing its running means
+    // (GridRenderPlane::addRay semantics, bit-exact against the CPU restatement)
+    void render(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays, int depth_max,
+                uint64_t seed) {
+        Flat f;
+        flatten(scene, f);
+        if (!has_scene_ || !(f == last_)) {
+            has_scene_ = false;
+            if (ipt_upload_scene(ctx_, &f.sc) != IPT_OK) throw std::runtime_error(ipt_last_error(ctx_));
+            last_ = std::move(f);
+            last_.sc.lights = last_.lights.data();
+            last_.sc.spheres = last_.spheres.empty() ? nullptr : last_.spheres.data();
+            has_scene_ = true;
+            ++uploads_;
+        }
+        ipt_params p{};
+        p.width = (int)plane.width;
+        p.height = (int)plane.height;
+        p.spp = spp;
+        p.spp_offset = spp_offset;
+        p.n_rays = n_rays;
+        p.depth_max = depth_max;
+        p.seed = seed;
+        // GridRenderPlane counts in size_t; the library in uint32 (< 2^32 passes)
+        std::vector<uint32_t> cnt(plane.pixel_counters.begin(), plane.pixel_counters.end());
+        std::vector<float> pmax(plane.pixels.size(), 0.0f);
+        ipt_image img{plane.pixels.data(), cnt.data(), nullptr, pmax.data()};
+        if (ipt_render(ctx_, &p, &img) != IPT_OK) throw std::runtime_error(ipt_last_error(ctx_));
+        std::copy(cnt.begin(), cnt.end(), plane.pixel_counters.begin());
+        for (float m : pmax) plane.max_value = std::max(plane.max_value, m);
+    }
+    int uploads() const { return uploads_; }
+
+private:
+    ipt_ctx* ctx_ = nullptr;
+    Flat last_;
+    bool has_scene_ = false;
+    int uploads_ = 0;
+};
+
+// The free-function form of INTEGRATION.md §1 on a process-wide renderer,
+// released by render_gpu_release() (call it before exit: the HIP runtime may
+// be torn down before static destructors run).
+static std::unique_ptr<GpuRenderer> g_renderer;
+
 void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
                         int depth_max, uint64_t seed) {
-    static ipt_ctx* ctx = nullptr;
-    if (!ctx && ipt_create(0, &ctx) != IPT_OK) throw std::runtime_error(ipt_last_error(nullptr));
-    std::vector<ipt_area_light> lights;
-    ipt_scene sc = flatten(scene, lights);
-    if (ipt_upload_scene(ctx, &sc) != IPT_OK) throw std::runtime_error(ipt_last_error(ctx));
-    ipt_params p{};
-    p.width = (int)plane.width;
-    p.height = (int)plane.height;
-    p.spp = spp;
-    p.spp_offset = spp_offset;
-    p.n_rays = n_rays;
-    p.depth_max = depth_max;
-    p.seed = seed;
-    std::vector<uint32_t> cnt(plane.pixel_counters.begin(), plane.pixel_counters.end());
-    std::vector<float> pmax(plane.pixels.size(), 0.0f);
-    ipt_image img{plane.pixels.data(), cnt.data(), nullptr, pmax.data()};
-    if (ipt_render(ctx, &p, &img) != IPT_OK) throw std::runtime_error(ipt_last_error(ctx));
-    std::copy(cnt.begin(), cnt.end(), plane.pixel_counters.begin());
-    for (float m : pmax) plane.max_value = std::max(plane.max_value, m);
+    if (!g_renderer) g_renderer = std::make_unique<GpuRenderer>(0);
+    g_renderer->render(scene, plane, spp, spp_offset, n_rays, depth_max, seed);
 }
+
+int render_gpu_uploads() { return g_renderer ? g_renderer->uploads() : 0; }
+
+void render_gpu_release() { g_renderer.reset(); }

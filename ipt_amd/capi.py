@@ -69,7 +69,7 @@ class Image(C.Structure):
                 ("pixel_max", C.c_void_p)]
 
 
-ABI_VERSION = 3  # include/ipt_capi.h IPT_ABI_VERSION
+ABI_VERSION = 4  # include/ipt_capi.h IPT_ABI_VERSION
 
 COUNTER_NAMES = ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
                  "iterations", "light_samples", "skipped", "sphere_frames", "light_traces",
@@ -85,7 +85,8 @@ class Counters(C.Structure):
 
 EXPORTED_SYMBOLS = (
     "ipt_abi_version", "ipt_last_error", "ipt_create", "ipt_destroy", "ipt_upload_scene",
-    "ipt_render", "ipt_render_device", "ipt_render_values", "ipt_get_counters",
+    "ipt_render", "ipt_render_device", "ipt_render_device_async", "ipt_render_wait", "ipt_render_values",
+    "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
     "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck", "ipt_smooth", "ipt_glare", "ipt_ddf_sample", "ipt_ddf_value",
     "ipt_philox",
@@ -117,7 +118,9 @@ def load(path: str | os.PathLike | None = None):
         raise IptError(IPT_E_DEVICE, f"{p} is not built; run __graft_entry__.build()")
     lib = C.CDLL(str(p))
     lib.ipt_abi_version.restype = C.c_int
-    if lib.ipt_abi_version() != ABI_VERSION:
+    # (IPT_ABI_COMPAT=1: A/B tooling loading an older variant library; the
+    # entry points it lacks are then unavailable)
+    if lib.ipt_abi_version() != ABI_VERSION and not os.environ.get("IPT_ABI_COMPAT"):
         raise IptError(IPT_E_INVALID, f"{p}: ABI {lib.ipt_abi_version()} != {ABI_VERSION}; rebuild")
     lib.ipt_last_error.restype = C.c_char_p
     lib.ipt_last_error.argtypes = [C.c_void_p]
@@ -127,6 +130,9 @@ def load(path: str | os.PathLike | None = None):
     lib.ipt_upload_scene.argtypes = [C.c_void_p, C.POINTER(Scene)]
     lib.ipt_render.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(Image)]
     lib.ipt_render_device.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(Image), C.c_void_p]
+    if hasattr(lib, "ipt_render_device_async"):
+        lib.ipt_render_device_async.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(Image), C.c_void_p]
+        lib.ipt_render_wait.argtypes = [C.c_void_p]
     lib.ipt_render_values.argtypes = [C.c_void_p, C.POINTER(Params), C.c_void_p, C.c_void_p]
     lib.ipt_get_counters.argtypes = [C.c_void_p, C.POINTER(Counters)]
     lib.ipt_reset_counters.argtypes = [C.c_void_p]
@@ -243,6 +249,21 @@ class Context:
         im = Image()
         im.pixels, im.counters, im.sums, im.pixel_max = pixels_ptr, counters_ptr, sums_ptr, max_ptr
         _check(self.lib, self.h, self.lib.ipt_render_device(self.h, C.byref(p), C.byref(im), stream))
+
+    def render_device_async(self, p: Params, pixels_ptr, counters_ptr, sums_ptr=None, max_ptr=None,
+                            stream=None):
+        """Queue the render (ipt_render_device_async); complete on `stream`'s
+        order or after wait()."""
+        im = Image()
+        im.pixels, im.counters, im.sums, im.pixel_max = pixels_ptr, counters_ptr, sums_ptr, max_ptr
+        _check(self.lib, self.h, self.lib.ipt_render_device_async(self.h, C.byref(p), C.byref(im), stream))
+
+    def wait(self):
+        _check(self.lib, self.h, self.lib.ipt_render_wait(self.h))
+
+    @property
+    def has_async(self) -> bool:
+        return hasattr(self.lib, "ipt_render_device_async")
 
     def counters(self) -> dict:
         c = Counters()

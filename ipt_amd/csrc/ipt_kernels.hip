@@ -107,6 +107,12 @@ struct KParams {
     const float2* __restrict__ frame_sc;  // frame_table_kernel: RotateDdf angle (sin, cos) by to.z
     const uint4* __restrict__ rg;         // IPT_RAYGEN: [total_units][2] raygen_kernel records
     int count;                            // raygen_kernel: accumulate the drift counter
+    // the launch's work pool is drained (its last chunk of units handed out):
+    // `seq` is stored to *drained (signal memory, or null), which the next
+    // launch's stream waits for (hipStreamWaitValue64), so that launch starts
+    // in this one's tail instead of beside it
+    unsigned long long* drained;
+    unsigned long long seq;
 };
 
 // floor(n / d) for 32-bit n, d >= 1 from a double reciprocal: the estimate's
@@ -549,8 +555,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 // (IPT_GRID_WAVE). Per wave iteration every walking lane steps one cell: the
 // (lane, item) pairs of the cells the lanes stand on are numbered by a wave
 // prefix sum and tested 64 at a time, one pair per lane (the lane that owns
-// pair p is found from a 64-byte LDS table of segment starts and a max-scan;
-// its ray is read with ds_bpermute), and each accepted t goes to its owner's
+// pair p is found by a ds_permute of the segment starts and a max-scan; its
+// ray is read with ds_bpermute), and each accepted t goes to its owner's
 // LDS slot as an atomic minimum of (t bits << 32 | item position). Within a
 // cell the positions are in original-index order (grid_build_spheres fills
 // each cell in index order) and accepted t are positive, so the slot ends as
@@ -563,7 +569,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <bool COUNT>
 __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool walking, vec3 o, vec3 d, int& cell,
                                                       vec3& tmx, float& best, int& bidx, int budget,
-                                                      unsigned long long* slots, uint8_t* own, int lane,
+                                                      unsigned long long* slots, int lane,
                                                       uint32_t& c_nodes, uint32_t& c_tests IPT_DIAG_PARAMS) {
     const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     auto lin_of = [&](int c) {
@@ -627,6 +633,7 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
         const int excl = incl - cnt;
         if (total > 0) {
             if (cnt > 0) slots[lane] = ~0ull;
+            wave_lds_sync();  // the clears before any lane's atomic minimum
             const int dk = s0 - excl;  // pair p of this lane tests item p + dk
             // one round: pairs base .. base + 63 (owner, its ray, the item)
             struct Pair {
@@ -636,10 +643,20 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
                 bool valid;
             };
             auto setup = [&](int base, Pair& q) {
-                own[lane] = 0;
-                if (cnt > 0 && excl < base + 64 && incl > base) own[excl > base ? excl - base : 0] = (uint8_t)(lane + 1);
-                wave_lds_sync();
-                q.src = wave_scan_max((int)own[lane]) - 1;
+                // the owner of pair base + lane, in one ds_permute (no LDS
+                // round trip): every lane whose segment starts before the
+                // round's end sends lane + 1 to its start (clamped to 0); of
+                // lanes sharing a start only the highest-numbered can own
+                // pairs (excl[L] == excl[L+1] means cnt[L] == 0), and the
+                // highest-numbered source is the one ds_permute keeps. The
+                // lanes starting beyond the round (a suffix: excl does not
+                // decrease) send to position 63, which then takes the last
+                // sender; a max-scan carries each start to the pairs after it.
+                const bool snd = excl < base + 64;
+                int r = __builtin_amdgcn_ds_permute((snd ? (excl > base ? excl - base : 0) : 63) << 2, lane + 1);
+                const uint64_t sm = __ballot(snd);
+                if (~sm && lane == 63) r = __popcll(sm);
+                q.src = wave_scan_max(r) - 1;
                 const int p = base + lane;
                 q.valid = p < total;
                 const int sl = q.valid ? q.src : lane;
@@ -963,9 +980,11 @@ __host__ __device__ constexpr int block_of(int lmode) {
     return (lmode == 9 || lmode == 10) ? kLatticeBlock : kBlock;
 }
 __host__ __device__ constexpr bool resumable_geom(int geom);
-// the wave-spread grid walk's per-lane LDS (IPT_GRID_WAVE): 8-byte slot + 1 byte
+// the wave-spread grid walk's per-lane LDS (IPT_GRID_WAVE): an 8-byte slot
 __host__ __device__ constexpr int walk_lds_words(int lmode, int geom) {
-    return (IPT_GRID_WAVE && resumable_geom(geom)) ? 2 * block_of(lmode) + block_of(lmode) / 4 : 0;
+    // (the two-cell walk keeps its 64-byte owner table per wave)
+    return (IPT_GRID_WAVE && resumable_geom(geom)) ? 2 * block_of(lmode) + (IPT_GRID_WAVE == 2 ? block_of(lmode) / 4 : 0)
+                                                   : 0;
 }
 __host__ __device__ constexpr int frame_stride(int lmode, int geom) {
     return ((lmode == 1 || lmode == 5 || lmode == 6) && walk_lds_words(lmode, geom) == 0) ? block_of(lmode) + 64
@@ -1283,7 +1302,14 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
     bool tracing = false;  // a resumable walk (sphere list or light BVH) is in progress
     float xlmix = 0.0f;    // light walk: the running UnionDdf light sum
     vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
-    int xrdepth = 0, xi = 0, xbidx = -1, xp = -1;
+    int xrdepth = 0, xi = 0, xbidx = -1;
+    // sphere-list walks (kRes) keep |li_pos - origin|^2 instead of li_pos
+    // (resolve's only use of it), and neither the origin nor the depth: the
+    // lane's node does not change while it walks, so they are (is_iter ?
+    // tpos : camera) and (is_iter ? tdepth + 1 : 0); the plane hit rides in
+    // xbidx as -2 - plane (-1: none), negative until a sphere wins (-7 VGPRs:
+    // the C3 instance fits 128 without spills)
+    float xli_y = 0.0f;
     bool xis_iter = false, xhas_li = false;
     float xmult = 0.0f, xli_pow = 0.0f, xbest = 0.0f;
     vec3 xtm = v3(0, 0, 0);  // grid walk: t of the next cell boundaries
@@ -1308,6 +1334,10 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                 unsigned long long base = 0;
                 if (lane == __ffsll((long long)needmask) - 1)
                     base = atomicAdd(kp.unit_counter, (unsigned long long)kPoolChunk);
+                    // (a vector store from one lane; the words only increase:
+                    // a slot's launches run one after another)
+                    if (kp.drained && base + (unsigned long long)kPoolChunk >= kp.total_units)
+                        __hip_atomic_store(kp.drained, kp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 base = __shfl(base, __ffsll((long long)needmask) - 1);
                 if ((unsigned long long)rank < avail)
                     my = pool_next + rank;
@@ -1735,7 +1765,7 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
         // the child's value (main.cpp:100-143) from its traces, then push it,
         // add it to the current node's sum, or finish the path
         auto resolve = [&](bool traced, float t, int prim, vec3 o, vec3 d, int depth, bool iter, float mult,
-                           bool has_li, vec3 li_pos, float li_pow) {
+                           bool has_li, float li_y, float li_pow) {
             float cv = 0.0f;
             bool push = false;
             vec3 si_pos = v3(0, 0, 0);
@@ -1750,8 +1780,9 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                     c_light += has_li ? 1u : 0u;
                 }
                 si_pos = o + d * t;
-                const vec3 ea = si_pos - o, eb = li_pos - o;
-                const float x = dot(ea, ea), y = dot(eb, eb);
+                // y = |li_pos - o|^2, computed by the caller
+                const vec3 ea = si_pos - o;
+                const float x = dot(ea, ea), y = li_y;
                 // longer(si_pos - o, li_pos - o), asked only where both hits exist
                 const bool need = has_li && has_si;
                 bool lg = x > y * 1.000001907f && y >= 1e-30f;
@@ -1888,7 +1919,8 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                         IPT_PHASE(9);
                         t = trace_geometry<COUNT, GEOM>(kp, xro, xrd, &prim, c_nodes, c_tests);
                     }
-                    resolve(xrdepth < kp.depth_max, t, prim, xro, xrd, xrdepth, xis_iter, mult, xhas_li, xli_pos,
+                    const vec3 eb = xli_pos - xro;
+                    resolve(xrdepth < kp.depth_max, t, prim, xro, xrd, xrdepth, xis_iter, mult, xhas_li, dot(eb, eb),
                             xli_pow);
                 }
             }
@@ -2024,21 +2056,22 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
             // child ray_power (main.cpp:100-143): the geometry trace, then resolve
             if (kRes && rdepth < kp.depth_max && (kp.n_nodes > 0 || kp.n_grid > 0)) {
                 // resumable walk: keep the ray and the light results, planes now
-                xro = ro;
                 xrd = rd;
-                xrdepth = rdepth;
                 xis_iter = is_iter;
                 xmult = mult;
                 xhas_li = has_li;
-                xli_pos = li_pos;
+                {
+                    const vec3 eb = li_pos - ro;
+                    xli_y = dot(eb, eb);
+                }
                 xli_pow = li_pow;
-                xp = -1;
-                xbidx = -1;
+                int xp = -1;
                 xi = 0;
                 xbest = inf_();
                 if (GEOM == IPT_GEOM_SPHERES_IN_BOX)
                     xbest = (IPT_BOXDIV && kp.box_inrange) ? trace_box_planes_only<true>(ro, rd, &xp)
                                                            : trace_box_planes_only<false>(ro, rd, &xp);
+                xbidx = -2 - xp;
                 if (kp.n_grid > 0) sphere_grid_init(kg, ro, rd, xi, xtm);
                 tracing = true;
             } else {
@@ -2049,44 +2082,46 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                     t = trace_geometry<COUNT, GEOM>(kp, ro, rd, &prim, c_nodes, c_tests);
                     IPT_STAMP_AT(10);  // mixture value + geometry trace
                 }
-                resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, li_pos, li_pow);
+                const vec3 eb = li_pos - ro;
+                resolve(rdepth < kp.depth_max, t, prim, ro, rd, rdepth, is_iter, mult, has_li, dot(eb, eb), li_pow);
             }
         }
         IPT_STAMP_AT(11);  // resolve + push
+        // (kRes) the walking ray's origin: the lane's node or the camera
+        const vec3 xo = xis_iter ? tpos : kp.cam_pos;
         if (kRes && IPT_GRID_WAVE && kp.n_grid > 0) {
             // the whole wave walks (the item tests are spread over its lanes)
             if (__ballot(tracing)) {
                 if constexpr (IPT_GRID_WAVE == 2)
-                    sphere_grid_walk_wave2<COUNT>(kg, tracing, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
+                    sphere_grid_walk_wave2<COUNT>(kg, tracing, xo, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
                                                   wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes, c_tests);
                 else
-                    sphere_grid_walk_wave<COUNT>(kg, tracing, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
-                                                 wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes,
-                                                 c_tests IPT_DIAG_ARGS);
+                    sphere_grid_walk_wave<COUNT>(kg, tracing, xo, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
+                                                 wslots + (tid & ~63), lane, c_nodes, c_tests IPT_DIAG_ARGS);
             }
             if (tracing && xi < 0) {
                 tracing = false;
                 if (IPT_GRID_WAVE != 2 && xbidx >= 0) xbidx = grid_item_index(kg, xbidx);  // item position -> original index
-                resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : xp, xro, xrd, xrdepth, xis_iter, xmult, xhas_li, xli_pos,
-                        xli_pow);
+                resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : -2 - xbidx, xo, xrd, xis_iter ? tdepth + 1 : 0, xis_iter,
+                        xmult, xhas_li, xli_y, xli_pow);
             }
         } else if (kRes && tracing) {
             IPT_PHASE(9);
             bool done;
             if (kp.n_grid > 0) {
-                sphere_grid_walk<COUNT, IPT_GRID_PIPE != 0>(kg, xro, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET, c_nodes,
+                sphere_grid_walk<COUNT, IPT_GRID_PIPE != 0>(kg, xo, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET, c_nodes,
                                                           c_tests IPT_DIAG_ARGS);
                 done = xi < 0;
             } else {
-                sphere_bvh_walk<COUNT>(kp, xro, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
+                sphere_bvh_walk<COUNT>(kp, xo, xrd, xi, xbest, xbidx, IPT_WALK_BUDGET, c_nodes, c_tests);
                 done = xi >= kp.n_nodes;
             }
             if (done) {
                 tracing = false;
                 if (IPT_GRID_PIPE && kp.n_grid > 0 && xbidx >= 0)
                     xbidx = grid_item_index(kg, xbidx);  // item position -> original index
-                resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : xp, xro, xrd, xrdepth, xis_iter, xmult, xhas_li, xli_pos,
-                        xli_pow);
+                resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : -2 - xbidx, xo, xrd, xis_iter ? tdepth + 1 : 0, xis_iter,
+                        xmult, xhas_li, xli_y, xli_pow);
             }
         }
         }  // !kResL
@@ -2481,6 +2516,38 @@ std::string g_err_global;
 
 }  // namespace
 
+// One set of per-launch work buffers (radiance, drift codes, raygen records,
+// drifted-pixel flags, the shard's candidate rows, the work-unit counter) with
+// its own stream for raygen + path kernel. Consecutive launches -- chunks of
+// one call and consecutive calls alike -- alternate between two slots, so a
+// launch's workgroups take the CUs its predecessor's tail leaves idle (lanes
+// out of paths while the longest trees finish); the
+// GridRenderPlane replays run on the caller's stream in call order, each after
+// its own path kernel (an event), so the image is accumulated exactly as by
+// sequential calls.
+struct WorkSlot {
+    float* d_values = nullptr;
+    uint8_t* d_codes = nullptr;
+    uint4* d_rg = nullptr;  // raygen_kernel records, 2 x 16 B per element
+    size_t work_cap = 0;    // elements
+    uint8_t* d_flags = nullptr;
+    size_t flags_cap = 0;
+    int* d_cand_rows = nullptr;
+    int* d_cand_of_row = nullptr;
+    int cand_cap_rows = 0, cand_cap_h = 0;
+    int plan[4] = {-1, -1, -1, -1};  // (H, tile_rows, n_shards, shard_id) whose rows are on the device
+    unsigned long long* d_unit = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;  // after the last reader of the slot's buffers (accumulate or host copies)
+    hipEvent_t path_end = nullptr;  // after its last path kernel
+    unsigned long long seq = 0;     // launch number of its last launch
+    bool used = false;
+};
+struct ChunkTiming {
+    hipEvent_t t0 = nullptr, t1 = nullptr;  // raygen start, path-kernel end (slot stream)
+    hipEvent_t a0 = nullptr, a1 = nullptr;  // accumulate (caller stream; null without an image)
+};
+
 struct ipt_ctx {
     int device = 0;
     int n_cu = 256;
@@ -2520,23 +2587,25 @@ struct ipt_ctx {
     int light_grid_on = 1;  // coplanar light lattices by cell lookup (IPT_LIGHT_GRID=0: the light BVH)
     vec3 cam_pos, cam_dir, cam_right, cam_up;
     int box_inrange = 0;
-    // work buffers
-    float* d_values = nullptr;
-    uint8_t* d_codes = nullptr;
-    uint4* d_rg = nullptr;  // raygen_kernel records, 2 x 16 B per element
-    size_t work_cap = 0;  // elements
-    uint8_t* d_flags = nullptr;
-    size_t flags_cap = 0;
-    int* d_cand_rows = nullptr;
-    int* d_cand_of_row = nullptr;
-    int cand_cap_rows = 0, cand_cap_h = 0;
-    unsigned long long* d_unit = nullptr;
+    // work buffers: two slots, used by consecutive launches in turn (WorkSlot)
+    WorkSlot slot[2];
+    unsigned next_slot = 0;
+    unsigned long long launch_seq = 0;
+    // [2] pool-drained words of the slots' launches (hipMallocSignalMemory),
+    // null where hipStreamWaitValue64 is unavailable: consecutive launches
+    // then run one after the other (event waits)
+    unsigned long long* d_drained = nullptr;
+    size_t chunk_cap_test = 0;  // IPT_TEST_CHUNK_UNITS: at most this many units per launch (tests)
+    // timing of the launches queued since the last drain (event sets from ev_pool)
+    std::vector<ChunkTiming> pending;
+    ChunkTiming prev{};  // the last processed launch (its path-end event bounds the next one's start)
+    std::vector<hipEvent_t> ev_pool;
+    float run_path_ms = 0.0f, run_acc_ms = 0.0f;
     unsigned long long* d_counters = nullptr;
     float* d_cos_a = nullptr;   // CosineDdf tables (cos_table_kernel): r 64 MiB,
                                 // (cos phi, sin phi) 128 MiB
     float2* d_cos_b = nullptr;
     float2* d_frame_sc = nullptr;  // frame_table_kernel (IPT_FRAME_TAB), 1 GiB
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_path_ms = 0.0f, last_acc_ms = 0.0f;
     int blocks_per_cu = 0;      // of the last path-kernel launch
     bool lattice_lds = true;    // IPT_LATTICE_LDS=0: the lattice instances with global records (tests)
@@ -2600,48 +2669,104 @@ int ensure_frame_table(ipt_ctx* ctx, hipStream_t st) {
 // Work buffers grow on demand. A buffer's capacity is dropped to 0 together
 // with the buffer, so a failed regrowth never leaves a stale capacity over a
 // null pointer.
-int ensure_work(ipt_ctx* ctx, size_t elems, size_t npix, int H, int n_cand) {
-    if (elems > ctx->work_cap) {
-        if (ctx->d_values) hipFree(ctx->d_values);
-        if (ctx->d_codes) hipFree(ctx->d_codes);
-        if (ctx->d_rg) hipFree(ctx->d_rg);
-        ctx->d_values = nullptr;
-        ctx->d_codes = nullptr;
-        ctx->d_rg = nullptr;
-        ctx->work_cap = 0;
+int ensure_work(ipt_ctx* ctx, WorkSlot& S, size_t elems, size_t npix, int H, int n_cand) {
+    // (the caller has waited for the slot's previous launch and its readers)
+    if (elems > S.work_cap) {
+        if (S.d_values) hipFree(S.d_values);
+        if (S.d_codes) hipFree(S.d_codes);
+        if (S.d_rg) hipFree(S.d_rg);
+        S.d_values = nullptr;
+        S.d_codes = nullptr;
+        S.d_rg = nullptr;
+        S.work_cap = 0;
         DevBuf<float> v;
         DevBuf<uint8_t> c;
         DevBuf<uint4> g;
         HIPCHECK(ctx, hipMalloc(&v.p, elems * sizeof(float)));
         HIPCHECK(ctx, hipMalloc(&c.p, elems));
         if (IPT_RAYGEN) HIPCHECK(ctx, hipMalloc(&g.p, elems * 2 * sizeof(uint4)));
-        ctx->d_values = v.release();
-        ctx->d_codes = c.release();
-        ctx->d_rg = g.release();
-        ctx->work_cap = elems;
+        S.d_values = v.release();
+        S.d_codes = c.release();
+        S.d_rg = g.release();
+        S.work_cap = elems;
     }
-    if (npix > ctx->flags_cap) {
-        if (ctx->d_flags) hipFree(ctx->d_flags);
-        ctx->d_flags = nullptr;
-        ctx->flags_cap = 0;
-        HIPCHECK(ctx, hipMalloc(&ctx->d_flags, npix));
-        ctx->flags_cap = npix;
+    if (npix > S.flags_cap) {
+        if (S.d_flags) hipFree(S.d_flags);
+        S.d_flags = nullptr;
+        S.flags_cap = 0;
+        HIPCHECK(ctx, hipMalloc(&S.d_flags, npix));
+        S.flags_cap = npix;
     }
-    if (n_cand > ctx->cand_cap_rows || H > ctx->cand_cap_h) {
-        if (ctx->d_cand_rows) hipFree(ctx->d_cand_rows);
-        if (ctx->d_cand_of_row) hipFree(ctx->d_cand_of_row);
-        ctx->d_cand_rows = nullptr;
-        ctx->d_cand_of_row = nullptr;
-        ctx->cand_cap_rows = ctx->cand_cap_h = 0;
+    if (n_cand > S.cand_cap_rows || H > S.cand_cap_h) {
+        if (S.d_cand_rows) hipFree(S.d_cand_rows);
+        if (S.d_cand_of_row) hipFree(S.d_cand_of_row);
+        S.d_cand_rows = nullptr;
+        S.d_cand_of_row = nullptr;
+        S.cand_cap_rows = S.cand_cap_h = 0;
+        S.plan[0] = -1;
         DevBuf<int> r, o;
         HIPCHECK(ctx, hipMalloc(&r.p, sizeof(int) * std::max(n_cand, 1)));
         HIPCHECK(ctx, hipMalloc(&o.p, sizeof(int) * std::max(H, 1)));
-        ctx->d_cand_rows = r.release();
-        ctx->d_cand_of_row = o.release();
-        ctx->cand_cap_rows = n_cand;
-        ctx->cand_cap_h = H;
+        S.d_cand_rows = r.release();
+        S.d_cand_of_row = o.release();
+        S.cand_cap_rows = n_cand;
+        S.cand_cap_h = H;
     }
     return IPT_OK;
+}
+
+hipEvent_t pool_event(ipt_ctx* ctx) {
+    if (!ctx->ev_pool.empty()) {
+        hipEvent_t e = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+void pool_return(ipt_ctx* ctx, ChunkTiming& c) {
+    for (hipEvent_t e : {c.t0, c.t1, c.a0, c.a1})
+        if (e) ctx->ev_pool.push_back(e);
+    c = ChunkTiming{};
+}
+
+// Adds the oldest pending launch's times to the running sums (waiting for
+// it): its path time counts from its own start or from its predecessor's end,
+// whichever is later, so overlapped launches sum to their span; then the
+// accumulate kernel's time.
+int settle_oldest(ipt_ctx* ctx) {
+    ChunkTiming c = ctx->pending.front();
+    ctx->pending.erase(ctx->pending.begin());
+    HIPCHECK(ctx, hipEventSynchronize(c.a1 ? c.a1 : c.t1));
+    float path = 0.0f, d = 0.0f, acc = 0.0f;
+    HIPCHECK(ctx, hipEventElapsedTime(&path, c.t0, c.t1));
+    if (ctx->prev.t1 && hipEventElapsedTime(&d, c.t0, ctx->prev.t1) == hipSuccess && d > 0.0f)
+        path = std::max(0.0f, path - d);
+    if (c.a1) HIPCHECK(ctx, hipEventElapsedTime(&acc, c.a0, c.a1));
+    ctx->run_path_ms += path;
+    ctx->run_acc_ms += acc;
+    pool_return(ctx, ctx->prev);
+    ctx->prev = c;
+    return IPT_OK;
+}
+
+// Waits for every queued launch and its readers; the launches' times since
+// the previous drain become ipt_last_kernel_ms's.
+int drain(ipt_ctx* ctx) {
+    int rc = IPT_OK;
+    for (WorkSlot& S : ctx->slot)
+        if (S.st && hipStreamSynchronize(S.st) != hipSuccess) rc = fail(ctx, IPT_E_DEVICE, "slot stream failed");
+    while (!ctx->pending.empty()) {
+        const int r = settle_oldest(ctx);
+        if (r && !rc) rc = r;
+    }
+    pool_return(ctx, ctx->prev);
+    if (ctx->run_path_ms > 0.0f || ctx->run_acc_ms > 0.0f) {
+        ctx->last_path_ms = ctx->run_path_ms;
+        ctx->last_acc_ms = ctx->run_acc_ms;
+    }
+    ctx->run_path_ms = ctx->run_acc_ms = 0.0f;
+    return rc;
 }
 
 bool owned_host(const ipt_params* p, int yi) {
@@ -2802,32 +2927,79 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
     {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-            size_t avail = free_b + ctx->work_cap * kUnitBytes;
+            size_t avail = free_b + (ctx->slot[0].work_cap + ctx->slot[1].work_cap) * kUnitBytes;
             const size_t tables = (ctx->d_cos_a ? 0 : ((size_t)3 << 26)) +
                                   (ctx->d_frame_sc || !frame_table_user(ctx->geometry_kind)
                                        ? 0 : kFrameTabEntries * sizeof(float2));
             avail = avail > tables ? avail - tables : 0;
-            budget = std::min(budget, std::max<size_t>(per_pass, avail / 4 * 3 / kUnitBytes));
+            // (two slots: consecutive launches hold a chunk each)
+            budget = std::min(budget, std::max<size_t>(per_pass, avail / 8 * 3 / kUnitBytes));
         }
     }
+    if (ctx->chunk_cap_test) budget = std::min(budget, std::max<size_t>(per_pass, ctx->chunk_cap_test));
     const size_t n_chunks = std::max<size_t>(1, ((size_t)p->spp * per_pass + budget - 1) / budget);
     int chunk = (int)std::max<size_t>(1, ((size_t)p->spp + n_chunks - 1) / n_chunks);
     while (chunk > 1 && (size_t)chunk * per_pass > budget) --chunk;
-    int rc = ensure_work(ctx, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
-    if (rc) return rc;
-    rc = ensure_cos_tables(ctx, st);
+    int rc = ensure_cos_tables(ctx, st);
     if (rc) return rc;
     if (frame_table_user(ctx->geometry_kind)) {  // path_kernel's frame builds
         rc = ensure_frame_table(ctx, st);
         if (rc) return rc;
     }
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice, st));
-    HIPCHECK(ctx, hipMemcpyAsync(ctx->d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice, st));
     const int susp = needed_susp(p);
+    if (susp > 8) return fail(ctx, IPT_E_UNSUPPORTED, "recursion deeper than 8 suspended levels");
     const bool count = (p->flags & IPT_FLAG_COUNTERS) != 0;
-    float path_ms = 0.0f, acc_ms = 0.0f;
     for (int s0 = 0; s0 < p->spp; s0 += chunk) {
         const int ns = std::min(chunk, p->spp - s0);
+        // this launch's slot; its previous launch and that launch's readers
+        // (accumulate, host copies) must be done before its buffers are
+        // regrown or rewritten: the slot stream waits for them on the device,
+        // the host only where it rewrites device memory itself
+        WorkSlot& S = ctx->slot[ctx->next_slot];
+        ctx->next_slot ^= 1u;
+        const bool grow = (size_t)chunk * per_pass > S.work_cap || (size_t)W * H > S.flags_cap ||
+                          n_cand > S.cand_cap_rows || H > S.cand_cap_h;
+        const int plan[4] = {H, p->tile_rows, p->n_shards, p->shard_id};
+        const bool replan = !std::equal(plan, plan + 4, S.plan);
+        if (S.used && (grow || replan)) HIPCHECK(ctx, hipEventSynchronize(S.done));
+        rc = ensure_work(ctx, S, (size_t)chunk * per_pass, (size_t)W * H, H, n_cand);
+        if (rc) return rc;
+        if (replan) {
+            // (synchronous copies: the host vectors do not outlive the call)
+            HIPCHECK(ctx, hipMemcpy(S.d_cand_rows, rows.data(), sizeof(int) * n_cand, hipMemcpyHostToDevice));
+            HIPCHECK(ctx, hipMemcpy(S.d_cand_of_row, of_row.data(), sizeof(int) * H, hipMemcpyHostToDevice));
+            std::copy(plan, plan + 4, S.plan);
+        }
+        if (S.used) HIPCHECK(ctx, hipStreamWaitEvent(S.st, S.done, 0));
+        // start in the predecessor's tail: once its pool is drained (or, without
+        // stream value waits, once it has finished)
+        const unsigned sidx = (unsigned)(&S - ctx->slot);
+        WorkSlot& P = ctx->slot[sidx ^ 1u];
+        if (P.used) {
+            if (ctx->d_drained)
+                HIPCHECK(ctx, hipStreamWaitValue64(S.st, ctx->d_drained + (sidx ^ 1u), P.seq, hipStreamWaitValueGte,
+                                                   ~0ull));
+            else
+                HIPCHECK(ctx, hipStreamWaitEvent(S.st, P.path_end, 0));
+        }
+        const unsigned long long seq = ++ctx->launch_seq;
+        // bounded timing backlog: settle launches far behind (they are done or
+        // nearly so; the queue of launches ahead is untouched)
+        while (ctx->pending.size() >= 8) {
+            rc = settle_oldest(ctx);
+            if (rc) return rc;
+        }
+        ChunkTiming tm;
+        tm.t0 = pool_event(ctx);
+        tm.t1 = pool_event(ctx);
+        if (img) {
+            tm.a0 = pool_event(ctx);
+            tm.a1 = pool_event(ctx);
+        }
+        if (!tm.t0 || !tm.t1 || (img && (!tm.a0 || !tm.a1))) {
+            pool_return(ctx, tm);
+            return fail(ctx, IPT_E_DEVICE, "hipEventCreate failed");
+        }
         KParams kp{};
         kp.W = W;
         kp.H = H;
@@ -2838,7 +3010,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.key0 = (uint32_t)p->seed;
         kp.key1 = (uint32_t)(p->seed >> 32);
         kp.n_cand = n_cand;
-        kp.cand_rows = ctx->d_cand_rows;
+        kp.cand_rows = S.d_cand_rows;
         kp.tile_rows = p->tile_rows;
         kp.n_shards = p->n_shards;
         kp.shard_id = p->shard_id;
@@ -2848,10 +3020,10 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.box_inrange = ctx->box_inrange;
         kp.inv_per_pass = 1.0 / (double)per_pass;
         kp.inv_w = 1.0 / (double)W;
-        kp.unit_counter = ctx->d_unit;
-        kp.values = ctx->d_values;
-        kp.codes = ctx->d_codes;
-        kp.flags = ctx->d_flags;
+        kp.unit_counter = S.d_unit;
+        kp.values = S.d_values;
+        kp.codes = S.d_codes;
+        kp.flags = S.d_flags;
         kp.counters = ctx->d_counters;
         kp.geometry_kind = ctx->geometry_kind;
         kp.n_lights = ctx->n_lights;
@@ -2904,35 +3076,49 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cos_a = ctx->d_cos_a;
         kp.cos_b = ctx->d_cos_b;
         kp.frame_sc = ctx->d_frame_sc;
-        kp.rg = ctx->d_rg;
+        kp.rg = S.d_rg;
         kp.count = count ? 1 : 0;
-        HIPCHECK(ctx, hipMemsetAsync(ctx->d_unit, 0, sizeof(unsigned long long), st));
-        HIPCHECK(ctx, hipMemsetAsync(ctx->d_flags, 0, (size_t)W * H, st));
-        // ev[0]..ev[1]: the path's per-sample work, raygen_kernel (render_sample's
-        // jitter, camera ray, Philox block 0; ~0.2 % of a C2 launch) and path_kernel
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[0], st));
+        kp.drained = ctx->d_drained ? ctx->d_drained + sidx : nullptr;
+        kp.seq = seq;
+        // the slot stream: t0..t1 is the path's per-sample work, raygen_kernel
+        // (render_sample's jitter, camera ray, Philox block 0; ~0.2 % of a C2
+        // launch) and path_kernel
+        const hipStream_t ss = S.st;
+        ctx->pending.push_back(tm);  // (settled by drain, also on an error below)
+        S.used = true;
+        HIPCHECK(ctx, hipMemsetAsync(S.d_unit, 0, sizeof(unsigned long long), ss));
+        HIPCHECK(ctx, hipMemsetAsync(S.d_flags, 0, (size_t)W * H, ss));
+        HIPCHECK(ctx, hipEventRecord(tm.t0, ss));
         if (IPT_RAYGEN) {
-            hipLaunchKernelGGL(raygen_kernel, dim3((unsigned)((kp.total_units + 255) / 256)), dim3(256), 0, st, kp);
+            hipLaunchKernelGGL(raygen_kernel, dim3((unsigned)((kp.total_units + 255) / 256)), dim3(256), 0, ss, kp);
             HIPCHECK(ctx, hipGetLastError());
         }
-        if (susp <= 4)
-            rc = launch_path<4>(ctx, kp, st, count);
-        else if (susp <= 8)
-            rc = launch_path<8>(ctx, kp, st, count);
-        else
-            return fail(ctx, IPT_E_UNSUPPORTED, "recursion deeper than 8 suspended levels");
+        rc = susp <= 4 ? launch_path<4>(ctx, kp, ss, count) : launch_path<8>(ctx, kp, ss, count);
         if (rc) return rc;
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[1], st));
+        HIPCHECK(ctx, hipEventRecord(tm.t1, ss));
+        HIPCHECK(ctx, hipEventRecord(S.path_end, ss));
+        S.seq = seq;
+        if (host_values) {  // [spp][H][W] (whole frames: per_pass == W * H)
+            HIPCHECK(ctx, hipMemcpyAsync(host_values + (size_t)s0 * per_pass, S.d_values, sizeof(float) * ns * per_pass,
+                                         hipMemcpyDeviceToHost, ss));
+            HIPCHECK(ctx, hipMemcpyAsync(host_codes + (size_t)s0 * per_pass, S.d_codes, ns * per_pass,
+                                         hipMemcpyDeviceToHost, ss));
+        }
+        if (!img) HIPCHECK(ctx, hipEventRecord(S.done, ss));
         if (img) {
+            // the GridRenderPlane replay: on the caller's stream, in call order,
+            // after this launch's path kernel
+            HIPCHECK(ctx, hipStreamWaitEvent(st, tm.t1, 0));
+            HIPCHECK(ctx, hipEventRecord(tm.a0, st));
             AParams ap{};
             ap.W = W;
             ap.H = H;
             ap.spp = ns;
             ap.n_cand = n_cand;
-            ap.cand_of_row = ctx->d_cand_of_row;
-            ap.values = ctx->d_values;
-            ap.codes = ctx->d_codes;
-            ap.flags = ctx->d_flags;
+            ap.cand_of_row = S.d_cand_of_row;
+            ap.values = S.d_values;
+            ap.codes = S.d_codes;
+            ap.flags = S.d_flags;
             ap.tile_rows = p->tile_rows;
             ap.n_shards = p->n_shards;
             ap.shard_id = p->shard_id;
@@ -2943,23 +3129,10 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
             dim3 grid((W + 255) / 256, H), block(256);
             hipLaunchKernelGGL(accumulate_kernel, grid, block, 0, st, ap);
             HIPCHECK(ctx, hipGetLastError());
+            HIPCHECK(ctx, hipEventRecord(tm.a1, st));
+            HIPCHECK(ctx, hipEventRecord(S.done, st));
         }
-        HIPCHECK(ctx, hipEventRecord(ctx->ev[2], st));
-        if (host_values) {  // [spp][H][W] (whole frames: per_pass == W * H)
-            HIPCHECK(ctx, hipMemcpyAsync(host_values + (size_t)s0 * per_pass, ctx->d_values, sizeof(float) * ns * per_pass,
-                                         hipMemcpyDeviceToHost, st));
-            HIPCHECK(ctx, hipMemcpyAsync(host_codes + (size_t)s0 * per_pass, ctx->d_codes, ns * per_pass,
-                                         hipMemcpyDeviceToHost, st));
-        }
-        HIPCHECK(ctx, hipEventSynchronize(ctx->ev[2]));
-        float a = 0, b = 0;
-        HIPCHECK(ctx, hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]));
-        HIPCHECK(ctx, hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]));
-        path_ms += a;
-        acc_ms += b;
     }
-    ctx->last_path_ms = path_ms;
-    ctx->last_acc_ms = acc_ms;
     return IPT_OK;
 }
 
@@ -3007,6 +3180,7 @@ int ipt_create(int hip_device, ipt_ctx** out) {
         if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) != hipSuccess) lds = 0;
         if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, hip_device) != hipSuccess) optin = 0;
         if (std::max(lds, optin) > 0) ctx->max_lds = (size_t)std::max(lds, optin);
+        (void)hipGetLastError();  // an unsupported attribute must not leave a sticky error behind
     }
     if (const char* e = std::getenv("IPT_BLOCKS_PER_CU")) ctx->bpc_override = std::atoi(e);  // profiling only
     if (const char* e = std::getenv("IPT_LNODES_LDS")) ctx->lnodes_lds = std::atoi(e) != 0;
@@ -3016,9 +3190,32 @@ int ipt_create(int hip_device, ipt_ctx** out) {
         delete ctx;
         return fail(nullptr, IPT_E_DEVICE, "stream creation failed");
     }
-    for (auto& e : ctx->ev) hipEventCreate(&e);
-    if (hipMalloc(&ctx->d_unit, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps)) != hipSuccess ||
+    if (const char* e = std::getenv("IPT_TEST_CHUNK_UNITS")) ctx->chunk_cap_test = (size_t)std::atoll(e);  // tests
+    {
+        int wv = 0;
+        void* d = nullptr;
+        if (!std::getenv("IPT_NO_TAIL_OVERLAP") &&
+            hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, hip_device) == hipSuccess && wv &&
+            hipExtMallocWithFlags(&d, 2 * sizeof(unsigned long long), hipMallocSignalMemory) == hipSuccess) {
+            ctx->d_drained = static_cast<unsigned long long*>(d);
+            const unsigned long long zero[2] = {0, 0};
+            if (hipMemcpy(d, zero, sizeof zero, hipMemcpyDefault) != hipSuccess) {
+                (void)hipFree(d);
+                ctx->d_drained = nullptr;
+            }
+        }
+        (void)hipGetLastError();  // (probes that failed leave no sticky error for the caller's runtime)
+    }
+    for (WorkSlot& S : ctx->slot) {
+        if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&S.path_end, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&S.d_unit, sizeof(unsigned long long)) != hipSuccess) {
+            ipt_destroy(ctx);
+            return fail(nullptr, IPT_E_DEVICE, "work-slot stream / event / counter creation failed");
+        }
+    }
+    if (hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps)) != hipSuccess ||
         hipMalloc(&ctx->d_wall, sizeof(Frame) * 5) != hipSuccess) {
         ipt_destroy(ctx);
         return fail(nullptr, IPT_E_OOM, "hipMalloc failed");
@@ -3031,20 +3228,33 @@ int ipt_create(int hip_device, ipt_ctx** out) {
 void ipt_destroy(ipt_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
+    (void)drain(ctx);  // nothing queued may still use the buffers
     void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_lax, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
-                    ctx->d_values, ctx->d_codes, ctx->d_rg, ctx->d_flags, ctx->d_cand_rows,
-                    ctx->d_cand_of_row, ctx->d_unit, ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
+                    ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
                     ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_frame_sc};
     for (void* b : bufs)
         if (b) hipFree(b);
-    for (auto& e : ctx->ev)
-        if (e) hipEventDestroy(e);
+    for (WorkSlot& S : ctx->slot) {
+        void* sb[] = {S.d_values, S.d_codes, S.d_rg, S.d_flags, S.d_cand_rows, S.d_cand_of_row, S.d_unit};
+        for (void* b : sb)
+            if (b) hipFree(b);
+        if (S.done) hipEventDestroy(S.done);
+        if (S.path_end) hipEventDestroy(S.path_end);
+        if (S.st) hipStreamDestroy(S.st);
+    }
+    for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);
+    if (ctx->d_drained) hipFree(ctx->d_drained);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (!ctx) return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    {
+        const int rc = drain(ctx);  // queued launches read the scene being replaced
+        if (rc) return rc;
+    }
     ctx->has_scene = false;  // any failure below leaves no scene (ipt_capi.h)
     if (!s) return fail(ctx, IPT_E_INVALID, "scene is NULL");
     if (s->geometry_kind < IPT_GEOM_SPHERE_IN_BOX || s->geometry_kind > IPT_GEOM_SMALLPT)
@@ -3278,13 +3488,25 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     return IPT_OK;
 }
 
-int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, void* hip_stream) {
+int ipt_render_device_async(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, void* hip_stream) {
     int rc = validate(ctx, p);
     if (rc) return rc;
     if (!img || !img->pixels || !img->counters) return fail(ctx, IPT_E_INVALID, "image pixels/counters are NULL");
     hipSetDevice(ctx->device);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
     return render_chunks(ctx, p, img, st, nullptr, nullptr);
+}
+
+int ipt_render_wait(ipt_ctx* ctx) {
+    if (!ctx) return IPT_E_INVALID;
+    hipSetDevice(ctx->device);
+    return drain(ctx);
+}
+
+int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, void* hip_stream) {
+    const int rc = ipt_render_device_async(ctx, p, img, hip_stream);
+    const int rw = ctx ? drain(ctx) : IPT_OK;
+    return rc ? rc : rw;
 }
 
 int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* himg) {
@@ -3307,7 +3529,8 @@ int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* himg) {
     if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(d.pixel_max, himg->pixel_max, npix * 4, hipMemcpyHostToDevice, st));
     rc = render_chunks(ctx, p, &d, st, nullptr, nullptr);
     if (rc) {
-        (void)hipStreamSynchronize(st);  // no copy may still read the buffers when they are freed
+        (void)drain(ctx);  // no kernel or copy may still use the buffers when they are freed
+        (void)hipStreamSynchronize(st);
         return rc;
     }
     HIPCHECK(ctx, hipMemcpyAsync(himg->pixels, d.pixels, npix * 4, hipMemcpyDeviceToHost, st));
@@ -3315,7 +3538,7 @@ int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* himg) {
     if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(himg->sums, d.sums, npix * 4, hipMemcpyDeviceToHost, st));
     if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(himg->pixel_max, d.pixel_max, npix * 4, hipMemcpyDeviceToHost, st));
     HIPCHECK(ctx, hipStreamSynchronize(st));
-    return IPT_OK;
+    return drain(ctx);
 }
 
 int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t* codes) {
@@ -3325,7 +3548,9 @@ int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t*
     if (p->n_shards > 1) return fail(ctx, IPT_E_UNSUPPORTED, "ipt_render_values renders whole frames");
     hipSetDevice(ctx->device);
     rc = render_chunks(ctx, p, nullptr, ctx->stream, values, codes);
+    const int rw = drain(ctx);  // the host copies run on the slot streams
     if (rc) return rc;
+    if (rw) return rw;
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     return IPT_OK;
 }
@@ -3343,6 +3568,7 @@ int ipt_shard_plan(const ipt_params* p, uint8_t* owned_rows, int32_t* cand_rows,
 int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
     if (!ctx || !out) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (const int rc = drain(ctx)) return rc;
     unsigned long long h[kNumCounters];
     HIPCHECK(ctx, hipMemcpy(h, ctx->d_counters, sizeof h, hipMemcpyDeviceToHost));
     out->paths = h[0];
@@ -3366,6 +3592,7 @@ int ipt_get_counters(ipt_ctx* ctx, ipt_counters* out) {
 int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n) {
     if (!ctx || !out || n < 0) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (const int rc = drain(ctx)) return rc;
     unsigned long long h[2 * kProfPhases + kStamps];
     HIPCHECK(ctx, hipMemcpy(h, ctx->d_counters + kNumCounters, sizeof h, hipMemcpyDeviceToHost));
     for (int i = 0; i < n && i < 2 * kProfPhases + kStamps; ++i) out[i] = h[i];
@@ -3375,6 +3602,7 @@ int ipt_get_profile(ipt_ctx* ctx, uint64_t* out, int n) {
 int ipt_reset_counters(ipt_ctx* ctx) {
     if (!ctx) return IPT_E_INVALID;
     hipSetDevice(ctx->device);
+    if (const int rc = drain(ctx)) return rc;
     HIPCHECK(ctx, hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps)));
     return IPT_OK;
 }

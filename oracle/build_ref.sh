@@ -75,11 +75,12 @@ fi
 
 # INTEGRATION.md §1's reference-side adapter (integration/render_gpu.cpp),
 # type-checked and linked against the reference's own headers and TUs. The
-# one change the adapter documents -- public accessors for AreaLight's private
-# x_axis / y_axis / type (lighting.h:20-23) -- is applied to a temporary copy
-# of lighting.h outside the repository (removed below; nothing of it is kept).
+# changes the adapter documents -- public accessors for AreaLight's private
+# x_axis / y_axis / type (lighting.h:20-23) and FractalSpheres' rs / cs
+# (FractalSpheres.h:13-14) -- are applied to temporary copies of the two
+# headers outside the repository (removed below; nothing of them is kept).
 # Output: oracle/_ref/adapter_check (runs the adapter on the reference's
-# make_scene_box(), tests/test_reference_adapter.py).
+# sample scenes, tests/test_reference_adapter.py).
 LIB_DIR="$HERE/../ipt_amd/lib"
 if [ -f "$LIB_DIR/libipt_hip.so" ]; then
   PATCH=$(mktemp -d)
@@ -87,6 +88,11 @@ if [ -f "$LIB_DIR/libipt_hip.so" ]; then
   sed 's|^\(    AreaLight(glm::vec3 origin.*\)$|    glm::vec3 xAxis() const { return x_axis; }\n    glm::vec3 yAxis() const { return y_axis; }\n    type_t lightType() const { return type; }\n\1|' \
     "$REF/src/lighting/lighting.h" > "$PATCH/lighting/lighting.h"
   grep -q "lightType()" "$PATCH/lighting/lighting.h" || { echo "build_ref: accessor patch did not apply"; rm -rf "$PATCH"; exit 1; }
+  # FractalSpheres keeps its sphere list private (FractalSpheres.h:13-14)
+  mkdir -p "$PATCH/geometry"
+  sed 's|^private:$|    const std::vector<float>\& radii() const { return rs; }\n    const std::vector<glm::vec3>\& centers() const { return cs; }\nprivate:|' \
+    "$REF/src/geometry/FractalSpheres.h" > "$PATCH/geometry/FractalSpheres.h"
+  grep -q "centers()" "$PATCH/geometry/FractalSpheres.h" || { echo "build_ref: accessor patch did not apply"; rm -rf "$PATCH"; exit 1; }
   rc=0
   "$CXX" -std=c++17 -O2 -DBOOST_POOLFWD_HPP -I"$PATCH" "${FLAGS[@]:3}" -I"$HERE/../include" \
     "$HERE/../integration/render_gpu.cpp" "$HERE/../integration/adapter_check.cpp" "${objs[@]}" \

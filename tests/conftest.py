@@ -14,6 +14,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running (exhaustive) checks")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first():
+    """torch carries its own HIP runtime beside /opt/rocm's (which
+    libipt_hip.so links); when both are in one process torch's must
+    initialise first, or it finds no GPU. Tests that put torch tensors
+    next to an ipt context rely on this order (bench.py has it too)."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 @pytest.fixture(scope="session")
 def oracle():
     import oracle_binding

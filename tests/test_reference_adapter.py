@@ -2,9 +2,10 @@
 compiled against the REFERENCE's own headers and linked with its own TUs
 (oracle/build_ref.sh -> oracle/_ref/adapter_check; the only change is the
 three AreaLight accessors the adapter documents, patched into a temporary
-copy of lighting.h). The check harness builds the scene with the reference's
-make_scene_box() and a reference GridRenderPlane, then calls
-render_samples_gpu twice (progressive passes).
+copy of lighting.h, and FractalSpheres' sphere-list accessors). The check
+harness builds each scene with the reference's own sample_scenes code and a
+reference GridRenderPlane, then calls render_samples_gpu twice (progressive
+passes).
 
 * CPU: the adapter type-checks and links (the binary exists whenever the
   reference tree is present) and, without a GPU, fails loudly with the
@@ -35,7 +36,7 @@ def _need_bin():
 
 def test_adapter_builds_against_reference_and_fails_loudly_without_gpu(tmp_path):
     _need_bin()
-    r = subprocess.run([str(BIN), str(W), str(H), str(SPP), str(CALLS), str(tmp_path / "a")],
+    r = subprocess.run([str(BIN), "box", str(W), str(H), str(SPP), str(CALLS), str(tmp_path / "a")],
                        capture_output=True, text=True, timeout=120)
     if r.returncode == 3:
         assert "no HIP device" in r.stderr or "gfx950" in r.stderr, r.stderr
@@ -44,16 +45,26 @@ def test_adapter_builds_against_reference_and_fails_loudly_without_gpu(tmp_path)
 
 
 @pytest.mark.gpu
-def test_adapter_renders_reference_plane_bit_exact(oracle, tmp_path):
+@pytest.mark.parametrize("scene", ["box", "lit_corner", "fractal", "smallpt", "square_lit_by_square"])
+def test_adapter_renders_reference_plane_bit_exact(oracle, tmp_path, scene):
+    """Every sample_scenes entry (sample_scenes.cpp:20-108), built by the
+    reference's own code and flattened by the adapter (AreaLight square and
+    triangle, SphereLight; GeometrySphereInBox, GeometryCorner,
+    FractalSpheres, GeometrySmallPt, GeometryFloor): the reference
+    GridRenderPlane after two progressive calls is bit-identical to the
+    oracle's replay, and the scene was uploaded once."""
     _need_bin()
-    r = subprocess.run([str(BIN), str(W), str(H), str(SPP), str(CALLS), str(tmp_path / "a")],
+    r = subprocess.run([str(BIN), scene, str(W), str(H), str(SPP), str(CALLS), str(tmp_path / "a")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     px = np.fromfile(tmp_path / "a.f32", np.float32)
     cnt = np.fromfile(tmp_path / "a.u32", np.uint32)
-    ov, oc = ob.render_values(scenes.make_scene_box(), capi.make_params(W, H, SPP * CALLS))
+    desc = getattr(scenes, f"make_scene_{scene}")()
+    ov, oc = ob.render_values(desc, capi.make_params(W, H, SPP * CALLS))
     ref = ob.accumulate(ov, oc)
     assert np.array_equal(cnt, ref["counters"])
     assert np.array_equal(px.view(np.uint32), ref["pixels"].view(np.uint32))
-    mx = float(r.stdout.split()[1])
+    out = r.stdout.split()
+    mx = float(out[out.index("max_value") + 1])
     assert np.float32(mx) == ref["pixel_max"].max()
+    assert int(out[out.index("uploads") + 1]) == 1  # unchanged scene: not re-uploaded
