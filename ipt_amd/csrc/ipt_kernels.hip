@@ -107,12 +107,6 @@ struct KParams {
     const float2* __restrict__ frame_sc;  // frame_table_kernel: RotateDdf angle (sin, cos) by to.z
     const uint4* __restrict__ rg;         // IPT_RAYGEN: [total_units][2] raygen_kernel records
     int count;                            // raygen_kernel: accumulate the drift counter
-    // the launch's work pool is drained (its last chunk of units handed out):
-    // `seq` is stored to *drained (signal memory, or null), which the next
-    // launch's stream waits for (hipStreamWaitValue64), so that launch starts
-    // in this one's tail instead of beside it
-    unsigned long long* drained;
-    unsigned long long seq;
 };
 
 // floor(n / d) for 32-bit n, d >= 1 from a double reciprocal: the estimate's
@@ -976,19 +970,25 @@ constexpr int kLightWords = (int)(sizeof(LightDev) / 4);
 // (kLightsGridA10L/A01L: the per-lane LDS is the same, the shared tables and
 // records are held once per CU instead of once per 256-thread workgroup).
 constexpr int kLatticeBlock = 1024;
-__host__ __device__ constexpr int block_of(int lmode) {
-    return (lmode == 9 || lmode == 10) ? kLatticeBlock : kBlock;
-}
 __host__ __device__ constexpr bool resumable_geom(int geom);
+// The sphere-list (resumable) instances run 64-thread workgroups: a persistent
+// launch's tail frees a CU slot per finished wave instead of per finished
+// 4-wave workgroup, so the next launch fills it sooner (C3 +2.2 %, 16-spp
+// progressive calls 0.964 -> 0.985 of one call); C2 keeps 256 (its frame
+// columns' ds_read2st64 stride, -1.2 % at 64).
+__host__ __device__ constexpr int block_of(int lmode, int geom) {
+    return (lmode == 9 || lmode == 10) ? kLatticeBlock : (resumable_geom(geom) ? IPT_RES_BLOCK : kBlock);
+}
 // the wave-spread grid walk's per-lane LDS (IPT_GRID_WAVE): an 8-byte slot
 __host__ __device__ constexpr int walk_lds_words(int lmode, int geom) {
     // (the two-cell walk keeps its 64-byte owner table per wave)
-    return (IPT_GRID_WAVE && resumable_geom(geom)) ? 2 * block_of(lmode) + (IPT_GRID_WAVE == 2 ? block_of(lmode) / 4 : 0)
+    return (IPT_GRID_WAVE && resumable_geom(geom)) ? 2 * block_of(lmode, geom) + (IPT_GRID_WAVE == 2 ? block_of(lmode, geom) / 4 : 0)
                                                    : 0;
 }
 __host__ __device__ constexpr int frame_stride(int lmode, int geom) {
-    return ((lmode == 1 || lmode == 5 || lmode == 6) && walk_lds_words(lmode, geom) == 0) ? block_of(lmode) + 64
-                                                                                        : block_of(lmode) + 8;
+    return ((lmode == 1 || lmode == 5 || lmode == 6) && walk_lds_words(lmode, geom) == 0 && block_of(lmode, geom) >= 256)
+               ? block_of(lmode, geom) + 64
+               : block_of(lmode, geom) + 8;
 }
 __host__ __device__ constexpr size_t scene_lds_words(int lmode, int geom) {
     return (size_t)walk_lds_words(lmode, geom) + 12 * (size_t)frame_stride(lmode, geom) +
@@ -1146,8 +1146,8 @@ __global__ __launch_bounds__(256) void raygen_kernel(const KParams kp) {
 }
 
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
-__global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
-    constexpr int kBlock = block_of(LMODE);  // this instance's workgroup size
+__global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE)) void path_kernel(const KParams kp) {
+    constexpr int kBlock = block_of(LMODE, GEOM);  // this instance's workgroup size
     extern __shared__ float lds[];
     // IPT_GRID_WAVE (resumable sphere-list instances): a 64-bit test slot and a
     // segment-start byte per lane in front of the stack
@@ -1334,10 +1334,6 @@ __global__ __launch_bounds__(block_of(LMODE), waves_per_simd(GEOM, LMODE)) void 
                 unsigned long long base = 0;
                 if (lane == __ffsll((long long)needmask) - 1)
                     base = atomicAdd(kp.unit_counter, (unsigned long long)kPoolChunk);
-                    // (a vector store from one lane; the words only increase:
-                    // a slot's launches run one after another)
-                    if (kp.drained && base + (unsigned long long)kPoolChunk >= kp.total_units)
-                        __hip_atomic_store(kp.drained, kp.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 base = __shfl(base, __ffsll((long long)needmask) - 1);
                 if ((unsigned long long)rank < avail)
                     my = pool_next + rank;
@@ -2540,7 +2536,7 @@ struct WorkSlot {
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr;  // after the last reader of the slot's buffers (accumulate or host copies)
     hipEvent_t path_end = nullptr;  // after its last path kernel
-    unsigned long long seq = 0;     // launch number of its last launch
+    unsigned long long total = 0;   // work units of its last launch
     bool used = false;
 };
 struct ChunkTiming {
@@ -2590,11 +2586,11 @@ struct ipt_ctx {
     // work buffers: two slots, used by consecutive launches in turn (WorkSlot)
     WorkSlot slot[2];
     unsigned next_slot = 0;
-    unsigned long long launch_seq = 0;
-    // [2] pool-drained words of the slots' launches (hipMallocSignalMemory),
-    // null where hipStreamWaitValue64 is unavailable: consecutive launches
-    // then run one after the other (event waits)
-    unsigned long long* d_drained = nullptr;
+    // a launch starts once its predecessor's work pool is drained (its unit
+    // counter reached its total: hipStreamWaitValue64 on that counter, in
+    // device memory); without stream value waits (or IPT_NO_TAIL_OVERLAP=1)
+    // once the predecessor has finished (an event)
+    bool gate_on_pool = false;
     size_t chunk_cap_test = 0;  // IPT_TEST_CHUNK_UNITS: at most this many units per launch (tests)
     // timing of the launches queued since the last drain (event sets from ev_pool)
     std::vector<ChunkTiming> pending;
@@ -2826,7 +2822,7 @@ int needed_susp(const ipt_params* p) {
 // dynamic LDS bytes of a path-kernel instance (the layout at the top of path_kernel)
 template <int MAXSUSP, int LMODE, int GEOM>
 size_t path_lds_bytes(const KParams& kp) {
-    constexpr int kBlock = block_of(LMODE);
+    constexpr int kBlock = block_of(LMODE, GEOM);
     const size_t cells = (size_t)kp.lg_nu * kp.lg_nv;
     return ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
             (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0) : 0) +
@@ -2838,7 +2834,7 @@ size_t path_lds_bytes(const KParams& kp) {
 
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
-    constexpr int kBlock = block_of(LMODE);
+    constexpr int kBlock = block_of(LMODE, GEOM);
     const size_t lds = path_lds_bytes<MAXSUSP, LMODE, GEOM>(kp);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2846,7 +2842,7 @@ int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     // inter-block waits, so an over-reported residency only queues blocks)
     int bpc = 0;
     HIPCHECK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds));
-    bpc = std::max(1, std::min(bpc, 8));
+    bpc = std::max(1, std::min(bpc, 2048 / kBlock));  // (at most 32 waves per CU)
     if (ctx->bpc_override > 0) bpc = std::min(bpc, ctx->bpc_override);  // IPT_BLOCKS_PER_CU (profiling)
     ctx->blocks_per_cu = bpc;
     dim3 grid(ctx->n_cu * bpc), block(kBlock);
@@ -2975,14 +2971,14 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         // stream value waits, once it has finished)
         const unsigned sidx = (unsigned)(&S - ctx->slot);
         WorkSlot& P = ctx->slot[sidx ^ 1u];
+        // (P's counter is reset only by P's next launch, which waits for this
+        // launch's pool in turn, so this wait cannot miss its value)
         if (P.used) {
-            if (ctx->d_drained)
-                HIPCHECK(ctx, hipStreamWaitValue64(S.st, ctx->d_drained + (sidx ^ 1u), P.seq, hipStreamWaitValueGte,
-                                                   ~0ull));
+            if (ctx->gate_on_pool)
+                HIPCHECK(ctx, hipStreamWaitValue64(S.st, P.d_unit, P.total, hipStreamWaitValueGte, ~0ull));
             else
                 HIPCHECK(ctx, hipStreamWaitEvent(S.st, P.path_end, 0));
         }
-        const unsigned long long seq = ++ctx->launch_seq;
         // bounded timing backlog: settle launches far behind (they are done or
         // nearly so; the queue of launches ahead is untouched)
         while (ctx->pending.size() >= 8) {
@@ -3078,8 +3074,6 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.frame_sc = ctx->d_frame_sc;
         kp.rg = S.d_rg;
         kp.count = count ? 1 : 0;
-        kp.drained = ctx->d_drained ? ctx->d_drained + sidx : nullptr;
-        kp.seq = seq;
         // the slot stream: t0..t1 is the path's per-sample work, raygen_kernel
         // (render_sample's jitter, camera ray, Philox block 0; ~0.2 % of a C2
         // launch) and path_kernel
@@ -3097,7 +3091,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         if (rc) return rc;
         HIPCHECK(ctx, hipEventRecord(tm.t1, ss));
         HIPCHECK(ctx, hipEventRecord(S.path_end, ss));
-        S.seq = seq;
+        S.total = kp.total_units;
         if (host_values) {  // [spp][H][W] (whole frames: per_pass == W * H)
             HIPCHECK(ctx, hipMemcpyAsync(host_values + (size_t)s0 * per_pass, S.d_values, sizeof(float) * ns * per_pass,
                                          hipMemcpyDeviceToHost, ss));
@@ -3192,19 +3186,15 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     }
     if (const char* e = std::getenv("IPT_TEST_CHUNK_UNITS")) ctx->chunk_cap_test = (size_t)std::atoll(e);  // tests
     {
+        // (measured: hipStreamWaitValue64 on hipMalloc memory releases the
+        // waiting stream ~0.6 us after a kernel's atomicAdd reaches the value,
+        // scripts/probes/waitvalue_probe.hip)
         int wv = 0;
-        void* d = nullptr;
-        if (!std::getenv("IPT_NO_TAIL_OVERLAP") &&
-            hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, hip_device) == hipSuccess && wv &&
-            hipExtMallocWithFlags(&d, 2 * sizeof(unsigned long long), hipMallocSignalMemory) == hipSuccess) {
-            ctx->d_drained = static_cast<unsigned long long*>(d);
-            const unsigned long long zero[2] = {0, 0};
-            if (hipMemcpy(d, zero, sizeof zero, hipMemcpyDefault) != hipSuccess) {
-                (void)hipFree(d);
-                ctx->d_drained = nullptr;
-            }
-        }
-        (void)hipGetLastError();  // (probes that failed leave no sticky error for the caller's runtime)
+        ctx->gate_on_pool = !std::getenv("IPT_NO_TAIL_OVERLAP") &&
+                            hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, hip_device) ==
+                                hipSuccess &&
+                            wv;
+        (void)hipGetLastError();  // (an unsupported query leaves no sticky error for the caller's runtime)
     }
     for (WorkSlot& S : ctx->slot) {
         if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
@@ -3243,7 +3233,6 @@ void ipt_destroy(ipt_ctx* ctx) {
         if (S.st) hipStreamDestroy(S.st);
     }
     for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);
-    if (ctx->d_drained) hipFree(ctx->d_drained);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }

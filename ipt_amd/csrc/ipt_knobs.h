@@ -7,7 +7,7 @@
 #pragma once
 
 #if !defined(IPT_AB_BUILD) &&                                                                           \
-    (defined(IPT_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
+    (defined(IPT_BLOCK) || defined(IPT_RES_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
      defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
@@ -20,6 +20,9 @@
 // ---- launch shape
 #ifndef IPT_BLOCK
 #define IPT_BLOCK 256  // threads per workgroup (4 waves; 128 / 512 measured -2 % / -7 %)
+#endif
+#ifndef IPT_RES_BLOCK
+#define IPT_RES_BLOCK 64  // threads per workgroup of the sphere-list instances (C3: 64 / 128 / 256 -> 15.13 / 14.90 / 14.80)
 #endif
 #ifndef IPT_WAVES_PER_SIMD
 #define IPT_WAVES_PER_SIMD 4  // __launch_bounds__ occupancy of the non-resumable instances

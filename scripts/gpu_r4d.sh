@@ -1,12 +1,10 @@
-# Tail-overlap gating: wait-value probe, async tests, async vs sync benches
+# Tail-overlap gating on the predecessor's unit counter: async tests, async vs sync benches, progressive callers
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 30 ./scripts/probes/waitvalue_probe > gpurun_out/r4d_probe.log 2>&1 || { echo "probe failed rc=$?"; cat gpurun_out/r4d_probe.log; exit 1; }
-cat gpurun_out/r4d_probe.log
 timeout -k 10 200 python -u -m pytest tests/test_gpu_async.py -x -q --timeout 100 --timeout-method thread -m gpu > gpurun_out/r4d_async.log 2>&1 || { echo "async tests failed"; tail -30 gpurun_out/r4d_async.log; exit 1; }
 tail -1 gpurun_out/r4d_async.log
-for c in c3 c2; do
+for c in c3 c2 c5; do
   for m in "" "--sync"; do
     timeout -k 10 200 python bench.py --config $c --steps 2 --warmup 1 --cpu-seconds 0 --no-counters $m > gpurun_out/r4d_$c$m.json 2> gpurun_out/r4d_$c$m.err || { echo "bench $c $m failed"; tail -5 gpurun_out/r4d_$c$m.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/r4d_$c$m.json'));print('$c', '$m', round(d['value'],3), d['config']['calls'])"

@@ -70,9 +70,8 @@ int main() {
     unsigned long long* dev = nullptr;
     hipMalloc(&dev, 8);
     test("hipMalloc", dev);
-    void* sig = nullptr;
-    hipError_t e = hipExtMallocWithFlags(&sig, 8, hipMallocSignalMemory);
-    std::printf("signal alloc -> %s\n", hipGetErrorString(e));
-    if (e == hipSuccess) test("signal", (unsigned long long*)sig);
+    // (hipMallocSignalMemory is host memory here (memoryType 1): a kernel's
+    // atomicAdd on it never released the waiting stream within 30 s on the
+    // MI355X box, so the library gates on device memory only)
     return 0;
 }
