@@ -292,7 +292,10 @@ def main():
     # the steps are queued (ipt_render_device_async: a step's path kernel takes
     # the CUs the previous step's tail leaves idle; the GridRenderPlane replays
     # stay in step order on `stream`) and waited for once
-    use_async = ctx.has_async and not args.sync
+    # (under rocprofv3 counter collection dispatches are serialised and a
+    # gated launch would never start: synchronous steps there)
+    profiled = any(k.startswith(("ROCPROF", "ROCPROFILER")) for k in os.environ)
+    use_async = ctx.has_async and not args.sync and not profiled
 
     def render_step(p):
         if use_async:

@@ -2538,6 +2538,7 @@ struct WorkSlot {
     hipEvent_t path_end = nullptr;  // after its last path kernel
     unsigned long long total = 0;   // work units of its last launch
     bool used = false;
+    bool idle = true;  // its last launch is known complete (a drain since): nothing to wait for
 };
 struct ChunkTiming {
     hipEvent_t t0 = nullptr, t1 = nullptr;  // raygen start, path-kernel end (slot stream)
@@ -2750,8 +2751,11 @@ int settle_oldest(ipt_ctx* ctx) {
 // the previous drain become ipt_last_kernel_ms's.
 int drain(ipt_ctx* ctx) {
     int rc = IPT_OK;
-    for (WorkSlot& S : ctx->slot)
+    for (WorkSlot& S : ctx->slot) {
         if (S.st && hipStreamSynchronize(S.st) != hipSuccess) rc = fail(ctx, IPT_E_DEVICE, "slot stream failed");
+        if (S.used && S.done && hipEventSynchronize(S.done) != hipSuccess) rc = fail(ctx, IPT_E_DEVICE, "slot readers failed");
+        S.idle = true;  // (synchronous calls therefore queue no stream value waits)
+    }
     while (!ctx->pending.empty()) {
         const int r = settle_oldest(ctx);
         if (r && !rc) rc = r;
@@ -2973,7 +2977,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         WorkSlot& P = ctx->slot[sidx ^ 1u];
         // (P's counter is reset only by P's next launch, which waits for this
         // launch's pool in turn, so this wait cannot miss its value)
-        if (P.used) {
+        if (P.used && !P.idle) {
             if (ctx->gate_on_pool)
                 HIPCHECK(ctx, hipStreamWaitValue64(S.st, P.d_unit, P.total, hipStreamWaitValueGte, ~0ull));
             else
@@ -3080,6 +3084,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         const hipStream_t ss = S.st;
         ctx->pending.push_back(tm);  // (settled by drain, also on an error below)
         S.used = true;
+        S.idle = false;
         HIPCHECK(ctx, hipMemsetAsync(S.d_unit, 0, sizeof(unsigned long long), ss));
         HIPCHECK(ctx, hipMemsetAsync(S.d_flags, 0, (size_t)W * H, ss));
         HIPCHECK(ctx, hipEventRecord(tm.t0, ss));
