@@ -1210,7 +1210,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
     if (one_light(LMODE)) {
         LS.one = kp.lights[0];
         // held in VGPRs (+3.5 % C2; area and spow stay uniform)
-        if (IPT_RES_HOLD || !resumable_geom(GEOM)) {
+        if (IPT_LIGHT_HOLD && (IPT_RES_HOLD || !resumable_geom(GEOM))) {
             vgpr_hold(LS.one.P); vgpr_hold(LS.one.x); vgpr_hold(LS.one.y);
             vgpr_hold(LS.one.n); vgpr_hold(LS.one.inv.c[0]); vgpr_hold(LS.one.inv.c[1]); vgpr_hold(LS.one.inv.c[2]);
         }
