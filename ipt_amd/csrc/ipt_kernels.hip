@@ -3085,6 +3085,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         ctx->pending.push_back(tm);  // (settled by drain, also on an error below)
         S.used = true;
         S.idle = false;
+        S.total = 0;  // (until its kernel is queued: a successor must not wait on a launch that failed)
         HIPCHECK(ctx, hipMemsetAsync(S.d_unit, 0, sizeof(unsigned long long), ss));
         HIPCHECK(ctx, hipMemsetAsync(S.d_flags, 0, (size_t)W * H, ss));
         HIPCHECK(ctx, hipEventRecord(tm.t0, ss));
@@ -3094,9 +3095,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         }
         rc = susp <= 4 ? launch_path<4>(ctx, kp, ss, count) : launch_path<8>(ctx, kp, ss, count);
         if (rc) return rc;
+        S.total = kp.total_units;
         HIPCHECK(ctx, hipEventRecord(tm.t1, ss));
         HIPCHECK(ctx, hipEventRecord(S.path_end, ss));
-        S.total = kp.total_units;
         if (host_values) {  // [spp][H][W] (whole frames: per_pass == W * H)
             HIPCHECK(ctx, hipMemcpyAsync(host_values + (size_t)s0 * per_pass, S.d_values, sizeof(float) * ns * per_pass,
                                          hipMemcpyDeviceToHost, ss));
