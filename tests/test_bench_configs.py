@@ -44,3 +44,21 @@ def test_bench_workloads_match_baseline():
 def test_c3_default_run_is_the_whole_frame():
     _, _, _, spp_step, steps, _, _, _ = bench.CONFIGS["c3"]
     assert spp_step * steps == _parse(BASELINE[2])[2]
+
+
+def test_cpu_baseline_reports_threads_and_single_thread_rate():
+    """The CPU-baseline leg (the oracle, test infrastructure) states the
+    threads it used, the host's physical cores, a measured single-thread rate
+    and the full-host extrapolation beside the measured figure (CPU only,
+    a sub-second sample)."""
+    import types
+
+    a = types.SimpleNamespace(width=64, height=64, cpu_threads=2, cpu_sample=(16, 4), spp_per_step=1, steps=1,
+                              n_rays=4, depth_max=3, seed=20241223, cpu_seconds=0.3)
+    r = bench.cpu_baseline(a, bench.make_desc("box"))
+    assert r["cores"] == 2 and r["value"] > 0 and r["kind"] == "port"
+    assert r["single_thread_paths_per_s"] > 0 and r["thread_scaling"] > 0
+    phys = bench.physical_cores()
+    assert r["host_physical_cores"] == phys
+    if phys:
+        assert abs(r["full_host_extrapolated_Mpaths_s"] - r["single_thread_paths_per_s"] * phys / 1e6) < 1e-9
