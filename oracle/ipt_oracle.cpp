@@ -878,17 +878,18 @@ int ipt_oracle_render_rows_values(const ipt_scene* scene, const ipt_params* p, i
     for (int iy = row_phase; iy < H; iy += row_step) rows.push_back(iy);
     const int64_t nr = (int64_t)rows.size(), nrows = (int64_t)p->spp * nr;
     const int64_t nc = col_phase < W ? (W - 1 - col_phase) / col_step + 1 : 0;
+    // one path per work item: a sparse sample (C3's 128 paths per call) has
+    // fewer rows than threads, and path costs vary by orders of magnitude
     std::atomic<int64_t> next{0};
     if (n_threads <= 0) n_threads = (int)std::thread::hardware_concurrency();
     auto work = [&]() {
         for (;;) {
-            const int64_t r = next.fetch_add(1);
-            if (r >= nrows) break;
-            const int s = (int)(r / nr), q = (int)(r % nr);
-            for (int ix = col_phase, c = 0; ix < W; ix += col_step, ++c) {
-                int xi, yi;
-                values[((int64_t)s * nr + q) * nc + c] = oracle_pixel(cx, p, ix, rows[q], s, &xi, &yi);
-            }
+            const int64_t i = next.fetch_add(1);
+            if (i >= nrows * nc) break;
+            const int64_t r = i / nc;
+            const int s = (int)(r / nr), q = (int)(r % nr), c = (int)(i % nc);
+            int xi, yi;
+            values[i] = oracle_pixel(cx, p, col_phase + c * col_step, rows[q], s, &xi, &yi);
         }
     };
     std::vector<std::thread> th;
