@@ -62,3 +62,22 @@ def test_cpu_baseline_reports_threads_and_single_thread_rate():
     assert r["host_physical_cores"] == phys
     if phys:
         assert abs(r["full_host_extrapolated_Mpaths_s"] - r["single_thread_paths_per_s"] * phys / 1e6) < 1e-9
+
+
+def test_oracle_sample_renderer_is_thread_invariant():
+    """The CPU baseline's sampled renderer (one path per work item) gives the
+    full renderer's values at the sampled pixels, for any thread count."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import numpy as np
+    import oracle_binding as ob
+    from ipt_amd import capi, scenes
+
+    desc = scenes.make_scene_box()
+    p = capi.make_params(48, 40, 2, n_rays=4, depth_max=3, seed=7)
+    full, _ = ob.render_values(desc, p, n_threads=4)
+    ref = None
+    for th in (1, 3, 8):
+        v, rows, cols = ob.render_rows_values(desc, p, 7, 2, 5, 1, n_threads=th)
+        assert np.array_equal(v.view(np.uint32), full[:, rows][:, :, cols].view(np.uint32)), th
+        ref = v if ref is None else ref
+        assert np.array_equal(v.view(np.uint32), ref.view(np.uint32))
