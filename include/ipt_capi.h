@@ -211,10 +211,20 @@ int ipt_render_device(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, voi
 /* The same, returning once the launches are queued (the progressive loop of
    main.cpp:256-285 without a host wait per pass): the image is complete when
    `hip_stream` reaches the point after the call, or after ipt_render_wait.
-   The image buffers must stay valid until then. Calls into the same image on
-   the same stream accumulate exactly as sequential synchronous calls
-   (bit-identical). ipt_upload_scene, the counter calls and ipt_destroy wait
-   for queued work first. */
+   NULL is NOT the HIP null stream here but the context's own non-blocking
+   stream, which the caller's kernels are not ordered with: a caller that
+   passes NULL (torch's default-stream handle is 0) must call ipt_render_wait
+   before reading the image. The image buffers must stay valid until then.
+   Calls into the same image on the same stream accumulate exactly as
+   sequential synchronous calls (bit-identical). ipt_upload_scene, the counter
+   calls and ipt_destroy wait for queued work first.
+   Consecutive launches (the chunks of one call, or queued calls) start in
+   their predecessor's tail: a launch's stream waits (hipStreamWaitValue64) for
+   the predecessor's work pool to drain. Under a tool that serialises
+   dispatches for counter collection or thread trace (rocprofv3 --pmc / --att,
+   detected at ipt_create from ROCPROF_COUNTER_COLLECTION /
+   ROCPROF_ADVANCED_THREAD_TRACE), or with IPT_NO_TAIL_OVERLAP=1, a launch
+   waits for its predecessor's end instead (same images). */
 int ipt_render_device_async(ipt_ctx* ctx, const ipt_params* p, ipt_image* dev_img, void* hip_stream);
 /* Waits for every queued render; ipt_last_kernel_ms then holds the times of
    the launches since the previous wait (a synchronous render call waits). */

@@ -18,16 +18,27 @@ void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int
                         int depth_max, uint64_t seed);
 int render_gpu_uploads();
 void render_gpu_release();
+void render_samples_multi_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
+                              int depth_max, uint64_t seed, const std::vector<int>& devices, int tile_rows);
 
 int main(int argc, char** argv) {
     if (argc < 7) {
-        std::fprintf(stderr, "usage: adapter_check SCENE W H SPP_PER_CALL CALLS OUT_PREFIX [N_RAYS DEPTH]\n"
-                             "  SCENE: box | fractal | smallpt | square_lit_by_square | lit_corner\n");
+        std::fprintf(stderr, "usage: adapter_check SCENE W H SPP_PER_CALL CALLS OUT_PREFIX [N_RAYS DEPTH [DEVICES [TILE]]]\n"
+                             "  SCENE: box | fractal | smallpt | square_lit_by_square | lit_corner\n"
+                             "  DEVICES: comma-separated HIP devices, one context each (may repeat: 0,0,0)\n");
         return 2;
     }
     const std::string name = argv[1];
     const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), spp = std::atoi(argv[4]), calls = std::atoi(argv[5]);
     const int n_rays = argc > 7 ? std::atoi(argv[7]) : 16, depth = argc > 8 ? std::atoi(argv[8]) : 8;
+    std::vector<int> devices;
+    if (argc > 9)
+        for (const char* c = argv[9]; *c;) {
+            devices.push_back(std::atoi(c));
+            while (*c && *c != ',') ++c;
+            if (*c == ',') ++c;
+        }
+    const int tile = argc > 10 ? std::atoi(argv[10]) : 16;
     Scene scene;
     if (name == "box") scene = make_scene_box();
     else if (name == "fractal") scene = make_scene_fractal();
@@ -40,7 +51,12 @@ int main(int argc, char** argv) {
     }
     GridRenderPlane plane(W, H);
     try {
-        for (int c = 0; c < calls; ++c) render_samples_gpu(scene, plane, spp, c * spp, n_rays, depth, 20241223);
+        for (int c = 0; c < calls; ++c) {
+            if (devices.empty())
+                render_samples_gpu(scene, plane, spp, c * spp, n_rays, depth, 20241223);
+            else
+                render_samples_multi_gpu(scene, plane, spp, c * spp, n_rays, depth, 20241223, devices, tile);
+        }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "adapter_check: %s\n", e.what());
         render_gpu_release();

@@ -33,6 +33,8 @@
 #include <cstring>
 #include <memory>
 #include <stdexcept>
+#include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -152,9 +154,11 @@ public:
     GpuRenderer& operator=(const GpuRenderer&) = delete;
 
     // spp passes of render_sample into `plane`, continuing its running means
-    // (GridRenderPlane::addRay semantics, bit-exact against the CPU restatement)
+    // (GridRenderPlane::addRay semantics, bit-exact against the CPU restatement);
+    // with n_shards > 1 only the destination rows of tile shard `shard_id`
+    // (16-row tiles dealt round-robin, ipt_shard_plan) are rendered and written
     void render(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays, int depth_max,
-                uint64_t seed) {
+                uint64_t seed, int n_shards = 1, int shard_id = 0, int tile_rows = 16) {
         Flat f;
         flatten(scene, f);
         if (!has_scene_ || !(f == last_)) {
@@ -174,6 +178,11 @@ public:
         p.n_rays = n_rays;
         p.depth_max = depth_max;
         p.seed = seed;
+        if (n_shards > 1) {
+            p.tile_rows = tile_rows;
+            p.n_shards = n_shards;
+            p.shard_id = shard_id;
+        }
         // GridRenderPlane counts in size_t; the library in uint32 (< 2^32 passes)
         std::vector<uint32_t> cnt(plane.pixel_counters.begin(), plane.pixel_counters.end());
         std::vector<float> pmax(plane.pixels.size(), 0.0f);
@@ -202,6 +211,79 @@ void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int
     g_renderer->render(scene, plane, spp, spp_offset, n_rays, depth_max, seed);
 }
 
-int render_gpu_uploads() { return g_renderer ? g_renderer->uploads() : 0; }
 
-void render_gpu_release() { g_renderer.reset(); }
+// The N-device form (the reference renders with several threads into one
+// plane, src/main.cpp:256-285): one context per entry of `devices` (a device
+// may repeat), destination rows cut into `tile_rows`-row tiles dealt
+// round-robin to the contexts (ipt_params.n_shards / shard_id), each context
+// driven by its own host thread on a private copy of the plane, and the
+// owned rows of every shard copied back into the caller's plane at the end of
+// the call (every pixel has exactly one owner, so no arithmetic merges them).
+// Each shard traces only the samples that can land in its rows, with the same
+// (seed, pass, pixel) streams, so the plane is bit-identical to the
+// one-device render.
+static std::vector<std::unique_ptr<GpuRenderer>> g_multi;
+static std::vector<int> g_multi_devices;
+
+void render_samples_multi_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
+                              int depth_max, uint64_t seed, const std::vector<int>& devices, int tile_rows) {
+    const int n = (int)devices.size();
+    if (n == 0) throw std::runtime_error("render_samples_multi_gpu: no devices");
+    if (n == 1) {
+        render_samples_gpu(scene, plane, spp, spp_offset, n_rays, depth_max, seed);
+        return;
+    }
+    if (g_multi_devices != devices) {
+        g_multi.clear();
+        for (int d : devices) g_multi.push_back(std::make_unique<GpuRenderer>(d));
+        g_multi_devices = devices;
+    }
+    const size_t W = plane.width, H = plane.height;
+    std::vector<GridRenderPlane> part(n, plane);
+    std::vector<std::string> err(n);
+    std::vector<std::thread> th;
+    for (int k = 0; k < n; ++k)
+        th.emplace_back([&, k] {
+            try {
+                g_multi[k]->render(scene, part[k], spp, spp_offset, n_rays, depth_max, seed, n, k, tile_rows);
+            } catch (const std::exception& e) {
+                err[k] = e.what();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (int k = 0; k < n; ++k)
+        if (!err[k].empty()) throw std::runtime_error(err[k]);
+    ipt_params q{};
+    q.width = (int)W;
+    q.height = (int)H;
+    q.tile_rows = tile_rows;
+    q.n_shards = n;
+    std::vector<uint8_t> owned(H);
+    std::vector<int32_t> cand(H);
+    int32_t n_cand = 0;
+    for (int k = 0; k < n; ++k) {
+        q.shard_id = k;
+        if (ipt_shard_plan(&q, owned.data(), cand.data(), &n_cand) != IPT_OK)
+            throw std::runtime_error(ipt_last_error(nullptr));
+        for (size_t y = 0; y < H; ++y)
+            if (owned[y]) {
+                std::copy_n(part[k].pixels.begin() + y * W, W, plane.pixels.begin() + y * W);
+                std::copy_n(part[k].pixel_counters.begin() + y * W, W, plane.pixel_counters.begin() + y * W);
+            }
+        plane.max_value = std::max(plane.max_value, part[k].max_value);
+    }
+}
+
+// scene uploads of the most-uploaded context (1 when an unchanged scene is
+// rendered progressively)
+int render_gpu_uploads() {
+    int u = g_renderer ? g_renderer->uploads() : 0;
+    for (const auto& r : g_multi) u = std::max(u, r->uploads());
+    return u;
+}
+
+void render_gpu_release() {
+    g_renderer.reset();
+    g_multi.clear();
+    g_multi_devices.clear();
+}

@@ -70,6 +70,7 @@ class Image(C.Structure):
 
 
 ABI_VERSION = 4  # include/ipt_capi.h IPT_ABI_VERSION
+ABI_LAYOUT_COMPATIBLE = (3, 4)  # versions with this binding's struct layouts (IPT_ABI_COMPAT only)
 
 COUNTER_NAMES = ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
                  "iterations", "light_samples", "skipped", "sphere_frames", "light_traces",
@@ -118,10 +119,16 @@ def load(path: str | os.PathLike | None = None):
         raise IptError(IPT_E_DEVICE, f"{p} is not built; run __graft_entry__.build()")
     lib = C.CDLL(str(p))
     lib.ipt_abi_version.restype = C.c_int
-    # (IPT_ABI_COMPAT=1: A/B tooling loading an older variant library; the
-    # entry points it lacks are then unavailable)
-    if lib.ipt_abi_version() != ABI_VERSION and not os.environ.get("IPT_ABI_COMPAT"):
-        raise IptError(IPT_E_INVALID, f"{p}: ABI {lib.ipt_abi_version()} != {ABI_VERSION}; rebuild")
+    # (IPT_ABI_COMPAT=1: A/B tooling loading an older variant library; only
+    # the versions whose struct layouts this binding shares are accepted -- ABI
+    # 4 added entry points to 3 without touching a layout -- and the entry
+    # points an older library lacks are then unavailable)
+    v = lib.ipt_abi_version()
+    if v != ABI_VERSION:
+        if not (os.environ.get("IPT_ABI_COMPAT") and v in ABI_LAYOUT_COMPATIBLE):
+            raise IptError(IPT_E_INVALID, f"{p}: ABI {v} != {ABI_VERSION}; rebuild")
+        import warnings
+        warnings.warn(f"{p}: loading ABI {v} under IPT_ABI_COMPAT (binding is ABI {ABI_VERSION})")
     lib.ipt_last_error.restype = C.c_char_p
     lib.ipt_last_error.argtypes = [C.c_void_p]
     lib.ipt_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]

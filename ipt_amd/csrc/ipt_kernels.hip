@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <strings.h>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -2543,6 +2544,7 @@ struct WorkSlot {
 struct ChunkTiming {
     hipEvent_t t0 = nullptr, t1 = nullptr;  // raygen start, path-kernel end (slot stream)
     hipEvent_t a0 = nullptr, a1 = nullptr;  // accumulate (caller stream; null without an image)
+    bool recorded = false;  // every event of the launch was recorded (its queueing succeeded)
 };
 
 struct ipt_ctx {
@@ -2731,15 +2733,25 @@ void pool_return(ipt_ctx* ctx, ChunkTiming& c) {
 // it): its path time counts from its own start or from its predecessor's end,
 // whichever is later, so overlapped launches sum to their span; then the
 // accumulate kernel's time.
+// A launch whose queueing failed part-way (`recorded` false: its end events
+// were never recorded) is dropped without timing: its events go back to the
+// pool and the caller keeps the error message of the failure itself.
 int settle_oldest(ipt_ctx* ctx) {
     ChunkTiming c = ctx->pending.front();
     ctx->pending.erase(ctx->pending.begin());
-    HIPCHECK(ctx, hipEventSynchronize(c.a1 ? c.a1 : c.t1));
+    if (!c.recorded) {
+        pool_return(ctx, c);
+        return IPT_OK;
+    }
+    const hipError_t e = hipEventSynchronize(c.a1 ? c.a1 : c.t1);
     float path = 0.0f, d = 0.0f, acc = 0.0f;
-    HIPCHECK(ctx, hipEventElapsedTime(&path, c.t0, c.t1));
+    if (e != hipSuccess || hipEventElapsedTime(&path, c.t0, c.t1) != hipSuccess ||
+        (c.a1 && hipEventElapsedTime(&acc, c.a0, c.a1) != hipSuccess)) {
+        pool_return(ctx, c);
+        return fail(ctx, IPT_E_DEVICE, std::string("render launch failed: ") + hipGetErrorString(e != hipSuccess ? e : hipGetLastError()));
+    }
     if (ctx->prev.t1 && hipEventElapsedTime(&d, c.t0, ctx->prev.t1) == hipSuccess && d > 0.0f)
         path = std::max(0.0f, path - d);
-    if (c.a1) HIPCHECK(ctx, hipEventElapsedTime(&acc, c.a0, c.a1));
     ctx->run_path_ms += path;
     ctx->run_acc_ms += acc;
     pool_return(ctx, ctx->prev);
@@ -3082,7 +3094,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         // (render_sample's jitter, camera ray, Philox block 0; ~0.2 % of a C2
         // launch) and path_kernel
         const hipStream_t ss = S.st;
-        ctx->pending.push_back(tm);  // (settled by drain, also on an error below)
+        ctx->pending.push_back(tm);  // (settled by drain, also on an error below: unrecorded, untimed)
+        ChunkTiming& tmq = ctx->pending.back();
         S.used = true;
         S.idle = false;
         S.total = 0;  // (until its kernel is queued: a successor must not wait on a launch that failed)
@@ -3132,6 +3145,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
             HIPCHECK(ctx, hipEventRecord(tm.a1, st));
             HIPCHECK(ctx, hipEventRecord(S.done, st));
         }
+        tmq.recorded = true;
     }
     return IPT_OK;
 }
@@ -3194,9 +3208,20 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     {
         // (measured: hipStreamWaitValue64 on hipMalloc memory releases the
         // waiting stream ~0.6 us after a kernel's atomicAdd reaches the value,
-        // scripts/probes/waitvalue_probe.hip)
+        // scripts/probes/waitvalue_probe.hip). A tool that serialises the
+        // dispatches to collect counters or traces (rocprofv3 --pmc / --att,
+        // which export ROCPROF_COUNTER_COLLECTION / ROCPROF_ADVANCED_THREAD_TRACE
+        // to the profiled process) never released such a wait queued behind a
+        // serialised dispatch, and the wait has no timeout: then
+        // every launch is gated on its predecessor's path-end event instead
+        // (the same images; consecutive launches lose their tail overlap).
+        auto env_on = [](const char* n) {
+            const char* v = std::getenv(n);
+            return v && *v && std::strcmp(v, "0") != 0 && strcasecmp(v, "false") != 0 && strcasecmp(v, "off") != 0;
+        };
+        const bool serialising_tool = env_on("ROCPROF_COUNTER_COLLECTION") || env_on("ROCPROF_ADVANCED_THREAD_TRACE");
         int wv = 0;
-        ctx->gate_on_pool = !std::getenv("IPT_NO_TAIL_OVERLAP") &&
+        ctx->gate_on_pool = !env_on("IPT_NO_TAIL_OVERLAP") && !serialising_tool &&
                             hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, hip_device) ==
                                 hipSuccess &&
                             wv;

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <fstream>
 #include <functional>
+#include <thread>
 
 #include "../csrc/ipt_math.h"  // glm-order float arithmetic (vec3, cross, normalize)
 
@@ -372,6 +373,11 @@ void GpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
     q.depth_max = p.depth_max;
     q.seed = p.seed;
     q.flags = p.counters ? IPT_FLAG_COUNTERS : 0;
+    if (p.n_shards > 1) {
+        q.tile_rows = p.tile_rows;
+        q.n_shards = p.n_shards;
+        q.shard_id = p.shard_id;
+    }
     std::vector<uint32_t> cnt(n);
     for (size_t i = 0; i < n; ++i) {
         if (plane.pixel_counters[i] > 0xffffffffull - (size_t)std::max(p.spp, 0))
@@ -420,6 +426,81 @@ void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, const Render
     GpuRenderer r(device);
     r.upload(scene);
     r.render(plane, p);
+}
+
+MultiGpuRenderer::MultiGpuRenderer(const std::vector<int>& devices, int tile_rows) : tile_rows_(tile_rows) {
+    if (devices.empty()) throw IptError(IPT_E_INVALID, "MultiGpuRenderer: no devices");
+    if (tile_rows <= 0) throw IptError(IPT_E_INVALID, "MultiGpuRenderer: tile_rows must be positive");
+    for (int d : devices) r_.push_back(std::make_unique<GpuRenderer>(d));
+}
+
+void MultiGpuRenderer::upload(const Scene& s) {
+    FlatScene f = flatten(s);
+    for (auto& r : r_) check(r->handle(), ipt_upload_scene(r->handle(), &f.scene));
+}
+
+void MultiGpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
+    const int n = (int)r_.size();
+    if (n == 1) {
+        r_[0]->render(plane, p);
+        return;
+    }
+    const size_t W = plane.width, H = plane.height;
+    if (plane.pixels.size() != W * H || plane.pixel_counters.size() != W * H)
+        throw IptError(IPT_E_INVALID, "GridRenderPlane buffers do not match width*height");
+    std::vector<GridRenderPlane> part(n, plane);
+    std::vector<int> code(n, IPT_OK);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    for (int k = 0; k < n; ++k)
+        th.emplace_back([&, k] {
+            RenderParams q = p;
+            q.tile_rows = tile_rows_;
+            q.n_shards = n;
+            q.shard_id = k;
+            try {
+                r_[k]->render(part[k], q);
+            } catch (const IptError& e) {
+                code[k] = e.code;
+                msg[k] = e.what();
+            } catch (const std::exception& e) {
+                code[k] = IPT_E_DEVICE;
+                msg[k] = e.what();
+            }
+        });
+    for (auto& t : th) t.join();
+    for (int k = 0; k < n; ++k)
+        if (code[k] != IPT_OK) throw IptError(code[k], "shard " + std::to_string(k) + ": " + msg[k]);
+    ipt_params q{};
+    q.width = (int)W;
+    q.height = (int)H;
+    q.tile_rows = tile_rows_;
+    q.n_shards = n;
+    std::vector<uint8_t> owned(H);
+    std::vector<int32_t> cand(H);
+    int32_t n_cand = 0;
+    for (int k = 0; k < n; ++k) {
+        q.shard_id = k;
+        check(nullptr, ipt_shard_plan(&q, owned.data(), cand.data(), &n_cand));
+        for (size_t y = 0; y < H; ++y)
+            if (owned[y]) {
+                std::copy_n(part[k].pixels.begin() + y * W, W, plane.pixels.begin() + y * W);
+                std::copy_n(part[k].pixel_counters.begin() + y * W, W, plane.pixel_counters.begin() + y * W);
+            }
+        plane.max_value = std::max(plane.max_value, part[k].max_value);
+    }
+}
+
+void MultiGpuRenderer::last_kernel_ms(float* path_ms, float* accumulate_ms) const {
+    float pm = 0.0f, am = 0.0f;
+    for (const auto& r : r_) {
+        float a = 0.0f, b = 0.0f;
+        r->last_kernel_ms(&a, &b);
+        pm = std::max(pm, a);
+        am = std::max(am, b);
+    }
+    *path_ms = pm;
+    *accumulate_ms = am;
 }
 
 // ---------------------------------------------------------------- output

@@ -174,6 +174,11 @@ struct RenderParams {
     int depth_max = 8;    // main.cpp:94
     uint64_t seed = 20241223;
     bool counters = false;
+    // destination-row tile shard of this call (ipt_params.tile_rows / n_shards /
+    // shard_id): n_shards <= 1 renders the whole frame
+    int tile_rows = 16;
+    int n_shards = 1;
+    int shard_id = 0;
 };
 
 // Scene -> POD (ipt_scene). Owns the arrays the POD points into.
@@ -208,6 +213,30 @@ class GpuRenderer {
 
 // One-shot convenience (the INTEGRATION.md adapter's shape).
 void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, const RenderParams& p, int device = 0);
+
+// N contexts (one per entry of `devices`; a device may repeat), i.e. the
+// node's GPUs in one process. The reference renders with several worker
+// threads into one plane (main.cpp:256-285); here the destination rows are cut
+// into tile_rows-row tiles dealt round-robin to the contexts (ipt_shard_plan),
+// each context is driven by its own host thread on a private copy of the plane,
+// and at the end of the call the owned rows of every shard are copied into the
+// caller's plane (one owner per pixel, so nothing is summed). Each shard traces
+// only the samples that can land in its rows, with the same (seed, pass, pixel)
+// streams: the plane is bit-identical to GpuRenderer::render's.
+class MultiGpuRenderer {
+   public:
+    explicit MultiGpuRenderer(const std::vector<int>& devices, int tile_rows = 16);
+    void upload(const Scene& s);
+    void render(GridRenderPlane& plane, const RenderParams& p);
+    size_t size() const { return r_.size(); }
+    GpuRenderer& context(size_t k) { return *r_[k]; }
+    // the slowest context's kernel time of the last render (path, accumulate ms)
+    void last_kernel_ms(float* path_ms, float* accumulate_ms) const;
+
+   private:
+    std::vector<std::unique_ptr<GpuRenderer>> r_;
+    int tile_rows_;
+};
 
 // --------------------------------------------------------------- output
 // Gui's display normalisation (gui.cpp:11-16): (v / max)^(1/2.2), cut to [0, 1].

@@ -8,12 +8,16 @@
 //   ipt_render [--scene box|box_lights:K|spheres:N[:SEED]|random_lights:N[:SEED]]
 //              [--width 640] [--height 640] [--spp 16] [--passes 1]
 //              [--n-rays 16] [--depth 8] [--seed 20241223] [--device 0]
+//              [--devices 0,1,...,7 [--tile-rows 16]]
 //              [--out result.png] [--pfm pixels.pfm] [--counts counts.u32]
 //              [--pgm result.pgm] [--smooth SIDE] [--glare CUTOFF --glare-out glare.pfm]
 //
 // --smooth applies GridRenderPlane::smooth(SIDE) on the GPU before output;
 // --glare writes Gui's glare bloom of the plane (gui.cpp:28-52, GPU) as PFM;
 // --pgm writes main.cpp's contrast/gamma PGM (main.cpp:297-309).
+// --devices renders with one context per listed device (MultiGpuRenderer: the
+// rows cut into --tile-rows tiles dealt round-robin, owned rows assembled at
+// the end of each batch; a device may repeat); the image is the same bits.
 //
 // Prints one JSON line: scene, size, passes, Mpaths/s (whole call and kernel).
 #include <chrono>
@@ -22,6 +26,7 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <vector>
 
 #include "ipt_host.h"
 
@@ -31,6 +36,7 @@ namespace {
     std::fprintf(stderr,
                  "usage: ipt_render [--scene NAME] [--width W] [--height H] [--spp S] [--passes P]\n"
                  "                  [--n-rays N] [--depth D] [--seed X] [--device I]\n"
+                 "                  [--devices I,J,... [--tile-rows 16]]\n"
                  "                  [--out result.png] [--pfm pixels.pfm] [--counts counts.u32]\n"
                  "                  [--pgm result.pgm] [--smooth SIDE] [--glare CUTOFF --glare-out F.pfm]\n");
     std::exit(2);
@@ -41,7 +47,8 @@ int main(int argc, char** argv) {
     std::string scene_name = "box", out = "result.png", pfm, counts, pgm, glare_out;
     long smooth = 0;
     double glare = -1.0;
-    long width = 640, height = 640, spp = 16, passes = 1, n_rays = 16, depth = 8, device = 0;
+    long width = 640, height = 640, spp = 16, passes = 1, n_rays = 16, depth = 8, device = 0, tile_rows = 16;
+    std::vector<int> devices;
     unsigned long long seed = 20241223ull;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -58,6 +65,14 @@ int main(int argc, char** argv) {
         else if (a == "--depth") depth = std::atol(val());
         else if (a == "--seed") seed = std::strtoull(val(), nullptr, 0);
         else if (a == "--device") device = std::atol(val());
+        else if (a == "--devices") {
+            devices.clear();
+            for (const char* c = val(); *c;) {
+                devices.push_back(std::atoi(c));
+                while (*c && *c != ',') ++c;
+                if (*c == ',') ++c;
+            }
+        } else if (a == "--tile-rows") tile_rows = std::atol(val());
         else if (a == "--out") out = val();
         else if (a == "--pfm") pfm = val();
         else if (a == "--counts") counts = val();
@@ -70,8 +85,11 @@ int main(int argc, char** argv) {
     if (width <= 0 || height <= 0 || spp <= 0 || passes <= 0 || n_rays < 0 || depth < 0) usage("bad sizes");
     try {
         const ipt::Scene scene = ipt::make_scene_by_name(scene_name);
-        ipt::GpuRenderer gpu((int)device);
-        gpu.upload(scene);
+        if (devices.empty()) devices.push_back((int)device);
+        if (tile_rows <= 0) usage("bad --tile-rows");
+        ipt::MultiGpuRenderer gpus(devices, (int)tile_rows);
+        ipt::GpuRenderer& gpu = gpus.context(0);  // post-process runs on the first context
+        gpus.upload(scene);
         ipt::GridRenderPlane plane((size_t)width, (size_t)height);
         ipt::RenderParams p;
         p.spp = (int)spp;
@@ -82,9 +100,9 @@ int main(int argc, char** argv) {
         const auto t0 = std::chrono::steady_clock::now();
         for (long pass = 0; pass < passes; ++pass) {  // progressive: each batch continues the RNG stream
             p.spp_offset = (int)(pass * spp);
-            gpu.render(plane, p);
+            gpus.render(plane, p);
             float pm = 0.0f, am = 0.0f;
-            gpu.last_kernel_ms(&pm, &am);
+            gpus.last_kernel_ms(&pm, &am);
             kernel_ms += pm + am;
         }
         const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -107,9 +125,9 @@ int main(int argc, char** argv) {
         const double paths = (double)width * height * spp * passes;
         std::printf(
             "{\"scene\": \"%s\", \"width\": %ld, \"height\": %ld, \"spp\": %ld, \"passes\": %ld, "
-            "\"n_rays\": %ld, \"depth_max\": %ld, \"max_value\": %.9g, \"seconds\": %.4f, "
+            "\"n_rays\": %ld, \"depth_max\": %ld, \"devices\": %zu, \"max_value\": %.9g, \"seconds\": %.4f, "
             "\"Mpaths_per_s\": %.3f, \"kernel_Mpaths_per_s\": %.3f}\n",
-            scene_name.c_str(), width, height, spp, passes, n_rays, depth, (double)plane.max_value, secs,
+            scene_name.c_str(), width, height, spp, passes, n_rays, depth, gpus.size(), (double)plane.max_value, secs,
             paths / secs / 1e6, kernel_ms > 0 ? paths / (kernel_ms * 1e-3) / 1e6 : 0.0);
     } catch (const ipt::IptError& e) {
         std::fprintf(stderr, "ipt_render: error %d: %s\n", e.code, e.what());

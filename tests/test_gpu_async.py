@@ -117,12 +117,18 @@ def test_upload_between_queued_calls(gpu_ctx):
         _assert_same(_host(img), ob.accumulate(ov, oc))
 
 
+@pytest.mark.parametrize("gate", ["pool", "IPT_NO_TAIL_OVERLAP", "ROCPROF_COUNTER_COLLECTION"])
 @pytest.mark.parametrize("units", [1, 3000, 5000])
-def test_chunked_launches_bit_exact(oracle, monkeypatch, units):
+def test_chunked_launches_bit_exact(oracle, monkeypatch, units, gate):
     """IPT_TEST_CHUNK_UNITS caps a launch (at least one pass): a call split
     into many launches, alternating slots and overlapping, gives the same
-    image and the same per-sample values as the oracle."""
+    image and the same per-sample values as the oracle -- with the launches
+    gated on the predecessor's drained pool (the default) and on its end
+    event (IPT_NO_TAIL_OVERLAP, or a counter-collecting profiler detected at
+    ipt_create)."""
     monkeypatch.setenv("IPT_TEST_CHUNK_UNITS", str(units))
+    if gate != "pool":
+        monkeypatch.setenv(gate, "1")
     ctx = capi.Context(0)
     try:
         desc = scenes.make_scene_box()
@@ -163,3 +169,26 @@ def test_counters_after_queued_calls(gpu_ctx, oracle):
     _, _, o = ob.render_values(desc, capi.make_params(W, H, 3), 0, with_counters=True)
     for k in ("paths", "traced_rays", "iterations", "light_traces"):
         assert g[k] == o[k], (k, g[k], o[k])
+
+
+def test_chunked_call_under_counter_collection(tmp_path):
+    """A synchronous call split into several launches completes under
+    rocprofv3's counter collection (which serialises dispatches: a launch
+    gated on a stream value wait behind it was never released)
+    and stays bit-exact: the library must detect the tool and gate on events.
+    A hang is killed by the timeout and fails the test."""
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not Path(prof).exists():
+        pytest.skip("rocprofv3 not installed")
+    probe = Path(__file__).resolve().parent / "chunked_probe.py"
+    env = dict(__import__("os").environ, IPT_TEST_CHUNK_UNITS="3000", TMPDIR="/tmp")
+    r = subprocess.run(["timeout", "-s", "KILL", "150", prof, "--pmc", "SQ_WAVES", "--kernel-trace",
+                        "--output-format", "csv", "-d", str(tmp_path / "prof"), "-o", "run", "--",
+                        sys.executable, str(probe)], capture_output=True, text=True, env=env, timeout=200)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "bit-exact" in r.stdout

@@ -110,6 +110,33 @@ def test_cli_render_matches_oracle(gpu_ctx, oracle, tmp_path):
     assert (tmp_path / "r.png").read_bytes()[:4] == b"\x89PNG"
 
 
+@pytest.mark.parametrize("devices,tile", [("0,0", 16), ("0,0,0", 4)])
+def test_cli_multi_context_matches_oracle(gpu_ctx, oracle, tmp_path, devices, tile):
+    """The C++ N-context renderer (MultiGpuRenderer, ipt_render --devices):
+    one context per listed device (all on device 0 here), rows dealt in tiles,
+    owned rows assembled after every batch; two progressive batches at a
+    height that is not a multiple of tile_rows x N. Pixels and counters equal
+    the oracle's replay (the reference's threads, main.cpp:256-285, write one
+    plane; so do the contexts here)."""
+    import subprocess
+    import __graft_entry__ as ge
+    ge.build_host()
+    W, H, spp, passes = 40, 53, 2, 2
+    r = subprocess.run([str(ge.HOST_BIN), "--scene", "box", "--width", str(W), "--height", str(H),
+                        "--spp", str(spp), "--passes", str(passes), "--devices", devices, "--tile-rows", str(tile),
+                        "--out", "", "--pfm", str(tmp_path / "r.pfm"), "--counts", str(tmp_path / "r.u32")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    raw = (tmp_path / "r.pfm").read_bytes()
+    px = np.frombuffer(raw[raw.index(b"-1.0\n") + 5:], np.float32).reshape(H, W)[::-1].reshape(-1)
+    cnt = np.fromfile(tmp_path / "r.u32", np.uint32)
+    ov, oc = ob.render_values(scenes.make_scene_box(), capi.make_params(W, H, spp * passes))
+    ref = ob.accumulate(ov, oc)
+    assert np.array_equal(cnt, ref["counters"])
+    assert np.array_equal(_bits(px), _bits(ref["pixels"]))
+    assert '"devices": %d' % len(devices.split(",")) in r.stdout
+
+
 @pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs", "div_inrange_pairs", "longer_pairs",
                                 "udiv_exact_pairs", "sqrt_inrange", "frame_angle_sin", "frame_angle_cos"])
 def test_fast_math_exhaustive(gpu_ctx, fn):

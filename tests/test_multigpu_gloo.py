@@ -2,11 +2,11 @@
 and the frame-end assembly (ipt_amd/tiles.py, the code bench.py runs over
 RCCL).
 
-* test_two_rank_frame_assembly (CPU): each rank takes its tile plan from the
+* test_rank_frame_assembly (CPU, world_size 2 / 4 / 8, uneven shares): each rank takes its tile plan from the
   product (ipt_shard_plan), forms the GridRenderPlane rows it owns from the
   oracle's whole frame, and rank 0 assembles with tiles.assemble (one gather
   of owned rows); the result must equal the single-rank frame bit for bit.
-* test_two_rank_sharded_render_on_gpu (GPU): the same two-rank run with the
+* test_rank_sharded_render_on_gpu (GPU, world_size 2 / 4): the same run with the
   PRODUCT rendering each shard (both ranks on cuda:0, gloo for the frame
   end, as bench.py's IPT_BENCH_SHARE_GPU=1 rehearsal): the assembled frame
   must equal the whole-frame GPU render and the oracle's replay, bit for bit.
@@ -21,6 +21,10 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 W, H, SPP, TILE = 40, 48, 2, 8
+# (world, W, H, tile_rows) of the CPU assembly runs: H is not a multiple of
+# tile_rows * world at 4 and 8 ranks, so the ranks' padded shares are uneven
+# and the last tile is partial
+CPU_PLANS = [(2, 40, 48, 8), (4, 36, 53, 4), (8, 32, 77, 4)]
 
 
 def _free_port():
@@ -43,12 +47,12 @@ def _setup(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _state_of(img):
+def _state_of(img, h=H, w=W):
     return torch.from_numpy(np.stack([img[k].view(np.float32) for k in ("pixels", "counters", "sums", "pixel_max")])
-                            .reshape(4, H, W).copy())
+                            .reshape(4, h, w).copy())
 
 
-def _worker_cpu(rank, world, port, q):
+def _worker_cpu(rank, world, port, q, W=W, H=H, TILE=TILE):
     _setup(rank, world, port)
     import oracle_binding as ob
     from ipt_amd import capi, scenes, tiles
@@ -66,7 +70,7 @@ def _worker_cpu(rank, world, port, q):
                     yi = yn + ((int(codes[s, iy, ix]) >> 2) & 3) - 1
                     if yi in owned[rank]:
                         assert iy in cand, (rank, iy, yi)
-        full = _state_of(ob.accumulate(vals, codes))
+        full = _state_of(ob.accumulate(vals, codes), H, W)
         mine = torch.zeros_like(full)  # a rank's render writes only its owned rows
         mine[:, owned[rank]] = full[:, owned[rank]]
         tiles.assemble(dist, mine, owned, rank, host=True)
@@ -77,7 +81,7 @@ def _worker_cpu(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _worker_gpu(rank, world, port, q):
+def _worker_gpu(rank, world, port, q, W=W, H=H, TILE=TILE):
     _setup(rank, world, port)
     import oracle_binding as ob
     from ipt_amd import capi, scenes, tiles
@@ -107,7 +111,7 @@ def _worker_gpu(rank, world, port, q):
                 render(capi.make_params(W, H, SPP, spp_offset=s0), whole)
             torch.cuda.synchronize(dev)
             vals, codes = ob.render_values(desc, capi.make_params(W, H, 2 * SPP))
-            ref = _state_of(ob.accumulate(vals, codes))
+            ref = _state_of(ob.accumulate(vals, codes), H, W)
             got = state.cpu()
             q.put((wrote_outside, bool(torch.equal(got.view(torch.int32), whole.cpu().view(torch.int32))),
                    bool(torch.equal(got.view(torch.int32), ref.view(torch.int32)))))
@@ -118,11 +122,11 @@ def _worker_gpu(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def _run(target, world=2):
+def _run(target, world=2, extra=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
@@ -131,15 +135,20 @@ def _run(target, world=2):
     return [q.get(timeout=10) for _ in range(world if target is _worker_gpu else 2)]
 
 
-def test_two_rank_frame_assembly(oracle):
-    equal, partition = _run(_worker_cpu)
+@pytest.mark.parametrize("world,w,h,tile", CPU_PLANS)
+def test_rank_frame_assembly(oracle, world, w, h, tile):
+    """world_size 2 / 4 / 8 over gloo: the tile plan of every rank and the
+    frame-end gather of owned rows reproduce the single-rank frame bit for
+    bit, with uneven padded shares (the bench's N = 8 path on the CPU)."""
+    equal, partition = _run(_worker_cpu, world, (w, h, tile))
     assert equal is True
     assert partition is True  # every destination row owned exactly once
 
 
 @pytest.mark.gpu
-def test_two_rank_sharded_render_on_gpu(oracle):
-    res = _run(_worker_gpu)
+@pytest.mark.parametrize("world,w,h,tile", [(2, 40, 48, 8), (4, 36, 53, 4)])
+def test_rank_sharded_render_on_gpu(oracle, world, w, h, tile):
+    res = _run(_worker_gpu, world, (w, h, tile))
     full = [r for r in res if len(r) == 3]
     assert len(full) == 1
     assert not any(r[0] for r in res), "a shard wrote outside its rows"

@@ -68,3 +68,29 @@ def test_adapter_renders_reference_plane_bit_exact(oracle, tmp_path, scene):
     mx = float(out[out.index("max_value") + 1])
     assert np.float32(mx) == ref["pixel_max"].max()
     assert int(out[out.index("uploads") + 1]) == 1  # unchanged scene: not re-uploaded
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,devices,tile", [("box", "0,0,0", 4), ("lit_corner", "0,0", 16)])
+def test_adapter_multi_context_bit_exact(oracle, tmp_path, scene, devices, tile):
+    """render_samples_multi_gpu (the adapter's N-device form for the
+    reference's main, main.cpp:256-285): one context per listed device (all
+    on device 0 here), tile shards rendered by one host thread each, owned
+    rows copied into the reference's GridRenderPlane. Two progressive calls at
+    a height that is not a multiple of tile x N: bit-identical to the oracle,
+    each context uploaded the scene once."""
+    _need_bin()
+    Hm = 53
+    r = subprocess.run([str(BIN), scene, str(W), str(Hm), str(SPP), str(CALLS), str(tmp_path / "a"), "16", "8",
+                        devices, str(tile)], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    px = np.fromfile(tmp_path / "a.f32", np.float32)
+    cnt = np.fromfile(tmp_path / "a.u32", np.uint32)
+    desc = getattr(scenes, f"make_scene_{scene}")()
+    ov, oc = ob.render_values(desc, capi.make_params(W, Hm, SPP * CALLS))
+    ref = ob.accumulate(ov, oc)
+    assert np.array_equal(cnt, ref["counters"])
+    assert np.array_equal(px.view(np.uint32), ref["pixels"].view(np.uint32))
+    out = r.stdout.split()
+    assert np.float32(float(out[out.index("max_value") + 1])) == ref["pixel_max"].max()
+    assert int(out[out.index("uploads") + 1]) == 1
