@@ -97,6 +97,7 @@ struct KParams {
     const float4* __restrict__ lax;       // [n_lights][3] LightAx records (IPT_LIGHT_AX_REC)
     int lg_nu, lg_nv;
     float lg_u0, lg_v0, lg_icw, lg_ich;   // cell coordinates: (q - u0) * icw
+    float lg_e;                           // candidate margin in cells (LightGrid::e)
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
@@ -1300,6 +1301,10 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
     // the frame-entry prefetch pays where every lane iterates every step; in the
     // resumable instances (lanes parked in walks) it measured -5 % on C5
     constexpr int kFramePf = (kRes || kResL) ? 0 : IPT_FRAME_PF;
+    // certain light-sample skips taken within the step (the prologue below):
+    // the axis-aligned single-light instances, whose ranges are proven
+    constexpr bool kSkipAhead = IPT_SKIP_AHEAD && (LMODE == kLightsOneA10 || LMODE == kLightsOneA01 || grid_lights(LMODE)) &&
+                                !kRes && !kResL;
     bool tracing = false;  // a resumable walk (sphere list or light BVH) is in progress
     float xlmix = 0.0f;    // light walk: the running UnionDdf light sum
     vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
@@ -1501,10 +1506,17 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 // table line per cosine sample instead of two (computing r as
                 // well, or non-temporal gathers, measured slower: DESIGN.md 4.3)
                 tr = kp.cos_a[gcos ? gi_a : 0u];
-                float sp, cp;
-                sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
-                cs_c = cp;
-                cs_s = sp;
+                if constexpr (IPT_COSB_TAB) {
+                    // (cos phi, sin phi) gathered from the exact table as well
+                    const float2 cb = kp.cos_b[gcos ? gi_b : 0u];
+                    cs_c = cb.x;
+                    cs_s = cb.y;
+                } else {
+                    float sp, cp;
+                    sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
+                    cs_c = cp;
+                    cs_s = sp;
+                }
             }
         };
         auto prologue = [&]() {
@@ -1520,27 +1532,32 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             }
             const uint32_t j = k & 3u;  // = k - 4*blk: the window was shifted above
             const float r = u01(sel4(j, w.a0, w.a1, w.a2, w.a3));
-            int c = 0;
-            if (one_light(LMODE)) {
-                c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
-            } else if (global_lights(LMODE) && kp.cdf_lo) {
-                // the scan from the first index whose cdf exceeds r's bucket
-                // start floor(256 r)/256 (host table): every earlier entry is
-                // <= that start <= r, so the scan would pass it; a bucket holds
-                // at most 8 entries (else the table is not built)
-                c = cdf_lo_lds[(int)(r * 256.0f)];
-                while (c <= nl && !(r < LS.cdf(c))) ++c;
-            } else if ((global_lights(LMODE) || LMODE == kLightsAny) && kp.cdf_bsearch) {
-                // first c with r < cdf[c] (else nl+1): the scan's answer on a
-                // non-decreasing cdf (checked at upload)
-                int hi = nl + 1;
-                while (c < hi) {
-                    const int mid = (c + hi) >> 1;
-                    if (r < LS.cdf(mid)) hi = mid; else c = mid + 1;
+            // UnionDdf::sample's component: the first c with r < cdf[c] (ddf.cpp:142-153)
+            auto pick_of = [&](float r) {
+                int c = 0;
+                if (one_light(LMODE)) {
+                    c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+                } else if (global_lights(LMODE) && kp.cdf_lo) {
+                    // the scan from the first index whose cdf exceeds r's bucket
+                    // start floor(256 r)/256 (host table): every earlier entry is
+                    // <= that start <= r, so the scan would pass it; a bucket holds
+                    // at most 8 entries (else the table is not built)
+                    c = cdf_lo_lds[(int)(r * 256.0f)];
+                    while (c <= nl && !(r < LS.cdf(c))) ++c;
+                } else if ((global_lights(LMODE) || LMODE == kLightsAny) && kp.cdf_bsearch) {
+                    // first c with r < cdf[c] (else nl+1): the scan's answer on a
+                    // non-decreasing cdf (checked at upload)
+                    int hi = nl + 1;
+                    while (c < hi) {
+                        const int mid = (c + hi) >> 1;
+                        if (r < LS.cdf(mid)) hi = mid; else c = mid + 1;
+                    }
+                } else {
+                    while (c <= nl && !(r < LS.cdf(c))) ++c;
                 }
-            } else {
-                while (c <= nl && !(r < LS.cdf(c))) ++c;
-            }
+                return c;
+            };
+            const int c = pick_of(r);
             pick = c;
             if (c <= nl) {
                 const uint32_t r1 = sel4(j, w.a1, w.a2, w.a3, w.b0);
@@ -1559,6 +1576,50 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 k += 3;
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
+            }
+            if constexpr (kSkipAhead) {
+                // A light pick at a node on the lights' back side is a certain
+                // skip: DdfFromLight::sample returns vec3() when cosinus < 1e-5
+                // (lighting.cpp:125-134), and for these axis-aligned lights (one,
+                // or a coplanar lattice) the sampled point's normal-axis
+                // coordinate is P[2] whatever the two draws, so cosinus = n[2] *
+                // -RN(RN(P[2] - o[2]) * s) (s > 0: the instances' proven ranges)
+                // is <= 0 whenever n[2] * (o[2] - P[2]) <= 0. Such an iteration
+                // does nothing but consume its three draws and count
+                // (main.cpp:149-163), so the lane takes its next pick in the same
+                // step -- when the node has an iteration left and that pick's
+                // three draws are in the window without a shift (j <= 1: words
+                // j+3 .. j+5 <= 6, and k ends below 4*(blk+2)). Same draws, same
+                // order, same results; a lane on the back side of the lights
+                // spends one step instead of two on the pair.
+                float pz, nz;
+                if constexpr (grid_lights(LMODE)) {
+                    pz = kp.lg_pn;
+                    nz = kp.lg_nn;
+                } else {
+                    pz = LS.one.P.z;
+                    nz = LS.one.n.z;
+                }
+                const bool back = nz > 0.0f ? tpos.z <= pz : tpos.z >= pz;
+                if (c < nl && back && j <= 1u && ti + 1 < (kp.n_rays >> tdepth)) {
+                    ++ti;
+                    if (COUNT) { ++c_iter; ++c_lsamp; ++c_skip; }
+                    const bool j0 = j == 0u;
+                    const float r2 = u01(j0 ? w.a3 : w.b0);
+                    const int c2 = pick_of(r2);
+                    pick = c2;
+                    if (c2 <= nl) {
+                        const uint32_t q1 = j0 ? w.b0 : w.b1, q2 = j0 ? w.b1 : w.b2;
+                        u1 = u01(q1);
+                        u2 = u01(q2);
+                        gi_a = q1 >> 8;
+                        gi_b = q2 >> 8;
+                        gcos = c2 == nl;
+                        k += 3;
+                    } else {
+                        k += 1;
+                    }
+                }
             }
         };
         if (iter_lane) {
@@ -1986,7 +2047,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 const float u = (comp<XA>(ro) + comp<XA>(rd) * t - kp.lg_u0) * kp.lg_icw;
                 const float v = (comp<YA>(ro) + comp<YA>(rd) * t - kp.lg_v0) * kp.lg_ich;
                 int cand[4] = {-1, -1, -1, -1};
-                const float e = 0x1p-8f;
+                const float e = kp.lg_e;
                 if (u > -1.0f && u < (float)kp.lg_nu + 1.0f && v > -1.0f && v < (float)kp.lg_nv + 1.0f) {
                     const int i0 = (int)floorf(u - e), i1 = (int)floorf(u + e);
                     const int j0 = (int)floorf(v - e), j1 = (int)floorf(v + e);
@@ -1999,10 +2060,15 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     cand[2] = j1 != j0 ? cell(i0, j1) : -1;
                     cand[3] = (i1 != i0 && j1 != j0) ? cell(i1, j1) : -1;
                 }
-                // ascending index order (-1 = none sorts last as 0xffffffff)
+                // ascending index order (-1 = none sorts last as 0xffffffff);
+                // with the per-lattice margin a second candidate cell is rare
+                // (C5: ~1 lookup in 8 000), so the sorting network runs only in
+                // waves where some lane has one
                 uint32_t c0 = (uint32_t)cand[0], c1 = (uint32_t)cand[1], c2 = (uint32_t)cand[2], c3 = (uint32_t)cand[3];
                 auto cs = [](uint32_t& a, uint32_t& b) { const uint32_t lo = a < b ? a : b; b = a < b ? b : a; a = lo; };
-                cs(c0, c1); cs(c2, c3); cs(c0, c2); cs(c1, c3); cs(c1, c2);
+                if (__builtin_expect(__any((c1 & c2 & c3) != 0xffffffffu), 0)) {
+                    cs(c0, c1); cs(c2, c3); cs(c0, c2); cs(c1, c3); cs(c1, c2);
+                }
                 if (c0 != 0xffffffffu) light_step((int)c0);
                 if (c1 != 0xffffffffu) light_step((int)c1);
                 if (c2 != 0xffffffffu) light_step((int)c2);
@@ -3083,6 +3149,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.lg_v0 = ctx->lgrid.v0;
         kp.lg_icw = ctx->lgrid.icw;
         kp.lg_ich = ctx->lgrid.ich;
+        kp.lg_e = ctx->lgrid.e;
         kp.lg_pn = ctx->lgrid.pn;
         kp.lg_nn = ctx->lgrid.nn;
         kp.cos_a = ctx->d_cos_a;

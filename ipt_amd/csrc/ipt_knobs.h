@@ -13,7 +13,8 @@
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
-     defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG))
+     defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG) || \
+     defined(IPT_COSB_TAB) || defined(IPT_SKIP_AHEAD))
 #error "an ipt_knobs.h parameter is overridden: A/B builds must define IPT_AB_BUILD"
 #endif
 
@@ -67,6 +68,14 @@
 #endif
 #ifndef IPT_LIGHT_GRID
 #define IPT_LIGHT_GRID 1  // coplanar light lattices by cell lookup (kLightsGridA10/A01; C5 3x)
+#endif
+#ifndef IPT_SKIP_AHEAD
+#define IPT_SKIP_AHEAD 1  // single axis-aligned light: a certain light-sample skip and the next pick in one step
+#endif
+#ifndef IPT_COSB_TAB
+#define IPT_COSB_TAB 0  // non-resumable instances: CosineDdf's (cos phi, sin phi) gathered from the 128 MiB table
+                        // (C2 358 -> 256, C5 296 -> 256 Mpaths/s: the second random table line per cosine
+                        // iteration, round 5)
 #endif
 #ifndef IPT_LPF
 #define IPT_LPF 1  // lattice instances: the picked light's sample fields gathered in the prologue (C5 +2 %)

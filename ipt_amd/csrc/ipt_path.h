@@ -566,14 +566,31 @@ inline bool light_ranges_box(const LightDev& L, int na, const float cam[3]) {
 // pattern, the same normal and the same plane coordinate P[2] (so every
 // light's traceRay computes the same t and plane point q), and its rectangle
 // in the plane's (u, v) = (q[XA], q[YA]) one cell of a uniform lattice (within
-// 2^-12 of a cell on each edge), at most one light per cell. A light's exact
-// test passes only for q inside its rectangle up to a relative 2^-21, and the
-// kernel's cell coordinates of q are off by < 2^-13 cells for |u|, |v| <= 257,
-// so the lights of the cells within 2^-8 of (u, v) contain every hit.
+// 2^-12 of a cell on each edge), at most one light per cell. The kernel looks
+// a ray up by the cells within e of its cell coordinates (u, v), e the margin
+// below, computed per lattice.
+//
+// The margin. The light test and the lookup see the same float plane point q
+// (the same t, the same o + d*t). A light accepts q only within 2^-18 of a
+// cell beyond its rectangle: its lower edge is exact (RN(q - P) >= 0 iff
+// q >= P), its upper edge moves by the roundings of q - P and of the inverse
+// entry times it (relative < 2^-21 of the rectangle). The rectangle lies
+// within `dev` cells of its lattice cell (measured here in double). The
+// kernel's u = RN(RN(q - u0f) * icwf) is within eps = 2^-24 (|u0|/cw +
+// 3.01 (nu + 2)) cells of the exact (q - u0)/cw (u0f, icwf the float
+// parameters; three roundings relative to |u| <= nu + 2). So a hit light's
+// cell c has u in [c - m, c + 1 + m], m = dev + 2^-18 + eps, and with e >=
+// 2m + 2^-15 the kernel's RN(u -+ e) (rounding error < 2^-16 for |u| < 2^9)
+// still floors to c on the side where u left the cell. e is that bound
+// rounded up to a power of two, at least 2^-14; a lattice that would need more
+// than 2^-8 is not used. (C5's 16 x 16 lattice: dev 2^-18.5, e = 2^-14, so a
+// ray meets a second candidate cell in ~1 of 8 000 lookups instead of 1 of 64
+// with a fixed 2^-8.)
 struct LightGrid {
     int pattern = 0;  // axis_aligned_light() of every light; 0 = no lattice
     int nu = 0, nv = 0;
     float u0 = 0.0f, v0 = 0.0f, icw = 0.0f, ich = 0.0f, pn = 0.0f, nn = 0.0f;
+    float e = 0x1p-8f;       // candidate margin in cells (above)
     std::vector<int> cells;  // [nv][nu] light index, -1 = empty
 };
 inline bool light_grid_build(const LightDev* L, int nl, LightGrid& g) {
@@ -602,12 +619,16 @@ inline bool light_grid_build(const LightDev* L, int nl, LightGrid& g) {
     const double tol = 0x1p-12;
     std::vector<int> ci(nl), cj(nl);
     int nu = 0, nv = 0;
+    double dev = 0.0;  // largest deviation of a rectangle edge from its lattice line, in cells
     for (int i = 0; i < nl; ++i) {
         const double fi = (lu[i] - u0) / cw, fj = (lv[i] - v0) / ch;
         const double ri = __builtin_floor(fi + 0.5), rj = __builtin_floor(fj + 0.5);
-        if (!(__builtin_fabs(fi - ri) <= tol && __builtin_fabs((hu[i] - u0) / cw - (ri + 1.0)) <= tol &&
-              __builtin_fabs(fj - rj) <= tol && __builtin_fabs((hv[i] - v0) / ch - (rj + 1.0)) <= tol))
-            return false;
+        const double d[4] = {__builtin_fabs(fi - ri), __builtin_fabs((hu[i] - u0) / cw - (ri + 1.0)),
+                             __builtin_fabs(fj - rj), __builtin_fabs((hv[i] - v0) / ch - (rj + 1.0))};
+        for (double x : d) {
+            if (!(x <= tol)) return false;
+            dev = x > dev ? x : dev;
+        }
         if (ri < 0.0 || rj < 0.0 || ri >= 256.0 || rj >= 256.0) return false;
         ci[i] = (int)ri;
         cj[i] = (int)rj;
@@ -620,6 +641,18 @@ inline bool light_grid_build(const LightDev* L, int nl, LightGrid& g) {
           __builtin_fabs(vmax) <= 0x1p20 && cw >= 0x1p-12 * (__builtin_fabs(u0) + __builtin_fabs(umax)) &&
           ch >= 0x1p-12 * (__builtin_fabs(v0) + __builtin_fabs(vmax))))
         return false;  // cells small against their coordinates: rounding could exceed the margin
+    // the candidate margin (see LightGrid)
+    double m = 0.0;
+    for (int a = 0; a < 2; ++a) {
+        const double org = a == 0 ? u0 : v0, w = a == 0 ? cw : ch;
+        const int n = a == 0 ? nu : nv;
+        const double eps = 0x1p-24 * (__builtin_fabs(org) / w + 3.01 * (n + 2));
+        const double ma = dev + 0x1p-18 + eps;
+        m = ma > m ? ma : m;
+    }
+    double e = 0x1p-14;
+    while (e < 2.0 * m + 0x1p-15) e *= 2.0;
+    if (e > 0x1p-8) return false;
     g.cells.assign((size_t)nu * nv, -1);
     for (int i = 0; i < nl; ++i) {
         int& cell = g.cells[(size_t)ci[i] + (size_t)nu * cj[i]];
@@ -635,6 +668,7 @@ inline bool light_grid_build(const LightDev* L, int nl, LightGrid& g) {
     g.ich = (float)(1.0 / ch);
     g.pn = L[0].P.z;
     g.nn = L[0].n.z;
+    g.e = (float)e;
     return true;
 }
 

@@ -28,7 +28,8 @@ int main(int argc, char** argv) {
     }
     LightGrid g;
     const bool ok = light_grid_build(L.data(), n, g);
-    std::printf("lattice %d pattern %d nu %d nv %d\n", ok ? 1 : 0, g.pattern, g.nu, g.nv);
+    std::printf("lattice %d pattern %d nu %d nv %d e_log2 %d\n", ok ? 1 : 0, g.pattern, g.nu, g.nv,
+                ok ? (int)std::lround(std::log2(g.e)) : 0);
     if (!ok) return 0;
     const int XA = g.pattern == 1 ? 1 : 0, YA = 1 - XA;
     auto comp = [](vec3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); };
@@ -56,7 +57,7 @@ int main(int argc, char** argv) {
         const float v = (comp(o, YA) + comp(d, YA) * tt - g.v0) * g.ich;
         std::vector<int> cand;
         if (u > -1.0f && u < (float)g.nu + 1.0f && v > -1.0f && v < (float)g.nv + 1.0f) {
-            const float e = 0x1p-8f;
+            const float e = g.e;
             const int is[2] = {(int)std::floor(u - e), (int)std::floor(u + e)};
             const int js[2] = {(int)std::floor(v - e), (int)std::floor(v + e)};
             for (int a = 0; a < 2; ++a)
