@@ -98,6 +98,11 @@ struct KParams {
     int lg_nu, lg_nv;
     float lg_u0, lg_v0, lg_icw, lg_ich;   // cell coordinates: (q - u0) * icw
     float lg_e;                           // candidate margin in cells (LightGrid::e)
+    // skip-ahead (prologue): every light sample's point lies on the plane z =
+    // sa_pz and the light normal is (+-0, +-0, sa_nz): light picks at nodes
+    // with sa_nz * (sa_pz - z) >= 0 are certain skips (sa_on, host-checked)
+    int sa_on;
+    float sa_pz, sa_nz;
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
@@ -1303,8 +1308,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
     constexpr int kFramePf = (kRes || kResL) ? 0 : IPT_FRAME_PF;
     // certain light-sample skips taken within the step (the prologue below):
     // the axis-aligned single-light instances, whose ranges are proven
-    constexpr bool kSkipAhead = IPT_SKIP_AHEAD && (LMODE == kLightsOneA10 || LMODE == kLightsOneA01 || grid_lights(LMODE)) &&
-                                !kRes && !kResL;
+    constexpr bool kSkipAhead = IPT_SKIP_AHEAD && (one_light(LMODE) || grid_lights(LMODE)) && !kResL;
     bool tracing = false;  // a resumable walk (sphere list or light BVH) is in progress
     float xlmix = 0.0f;    // light walk: the running UnionDdf light sum
     vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
@@ -1557,11 +1561,48 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 }
                 return c;
             };
-            const int c = pick_of(r);
+            int c = pick_of(r);
+            uint32_t jj = j;  // the window offset of the iteration's pick (skip-ahead: j + 3)
+            if constexpr (kSkipAhead) {
+                // A light pick at a node on the lights' back side is a certain
+                // skip: DdfFromLight::sample returns vec3() when cosinus < 1e-5
+                // (lighting.cpp:125-134), and for these axis-aligned lights (one,
+                // or a coplanar lattice) the sampled point's normal-axis
+                // coordinate is P[2] whatever the two draws, so cosinus = n[2] *
+                // -RN(RN(P[2] - o[2]) * s) (+ signed zeros, generic light code;
+                // s = 1/|pos - o| >= 0: pos.z != o.z and |P[2]| >= 2^-32, so
+                // |pos - o|^2 >= 2^-112 does not underflow; an overflow gives
+                // s = 0 and cosinus = +-0) is <= 0 whenever n[2] * (P[2] - o[2])
+                // > 0 (sa_on: host-checked). Such an iteration does nothing but
+                // consume its three draws and count (main.cpp:149-163), so the
+                // lane takes the next iteration's pick (word j + 3) in the same
+                // step -- when the node has an iteration left and that pick's
+                // draws are in the window without a shift (j <= 1: words j+3 ..
+                // j+5 <= 6, and k ends below 4*(blk+2)). Same draws, same order,
+                // same results; a lane on the back side of the lights spends one
+                // step instead of two on the pair. (The draws below are then
+                // selected at offset jj = j + 3: one pick computation serves
+                // both cases.) (j = 2 as well -- words 5 .. 7, and the next
+                // step reading its pick at j = 4 after one shift -- measured
+                // +0.2 % on C2, -0.4 % on C5 and C3: not taken.)
+                // (o.z - P.z) * n.z < 0: the rounded difference keeps its sign
+                // and is zero only when o.z == P.z; an underflowed product is
+                // +-0, i.e. not taken (conservative)
+                const bool back = (tpos.z - kp.sa_pz) * kp.sa_nz < 0.0f;
+                if (kp.sa_on && c < nl && back && j <= 1u && ti + 1 < (kp.n_rays >> tdepth)) {
+                    ++ti;
+                    if (COUNT) { ++c_iter; ++c_lsamp; ++c_skip; }
+                    k += 3;
+                    jj = j + 3u;
+                    c = pick_of(u01(j == 0u ? w.a3 : w.b0));  // word j + 3
+                }
+            }
             pick = c;
             if (c <= nl) {
-                const uint32_t r1 = sel4(j, w.a1, w.a2, w.a3, w.b0);
-                const uint32_t r2 = sel4(j, w.a2, w.a3, w.b0, w.b1);
+                // words jj+1, jj+2 (jj <= 4 in the skip-ahead instances, else <= 3)
+                const bool hi = kSkipAhead && jj == 4u;
+                const uint32_t r1 = hi ? w.b1 : sel4(jj & 3u, w.a1, w.a2, w.a3, w.b0);
+                const uint32_t r2 = hi ? w.b2 : sel4(jj & 3u, w.a2, w.a3, w.b0, w.b1);
                 u1 = u01(r1);
                 u2 = u01(r2);
                 if (c == nl) {
@@ -1576,50 +1617,6 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 k += 3;
             } else {
                 k += 1;  // fall-through: defined as vec3() (reference UB, ddf.cpp:139)
-            }
-            if constexpr (kSkipAhead) {
-                // A light pick at a node on the lights' back side is a certain
-                // skip: DdfFromLight::sample returns vec3() when cosinus < 1e-5
-                // (lighting.cpp:125-134), and for these axis-aligned lights (one,
-                // or a coplanar lattice) the sampled point's normal-axis
-                // coordinate is P[2] whatever the two draws, so cosinus = n[2] *
-                // -RN(RN(P[2] - o[2]) * s) (s > 0: the instances' proven ranges)
-                // is <= 0 whenever n[2] * (o[2] - P[2]) <= 0. Such an iteration
-                // does nothing but consume its three draws and count
-                // (main.cpp:149-163), so the lane takes its next pick in the same
-                // step -- when the node has an iteration left and that pick's
-                // three draws are in the window without a shift (j <= 1: words
-                // j+3 .. j+5 <= 6, and k ends below 4*(blk+2)). Same draws, same
-                // order, same results; a lane on the back side of the lights
-                // spends one step instead of two on the pair.
-                float pz, nz;
-                if constexpr (grid_lights(LMODE)) {
-                    pz = kp.lg_pn;
-                    nz = kp.lg_nn;
-                } else {
-                    pz = LS.one.P.z;
-                    nz = LS.one.n.z;
-                }
-                const bool back = nz > 0.0f ? tpos.z <= pz : tpos.z >= pz;
-                if (c < nl && back && j <= 1u && ti + 1 < (kp.n_rays >> tdepth)) {
-                    ++ti;
-                    if (COUNT) { ++c_iter; ++c_lsamp; ++c_skip; }
-                    const bool j0 = j == 0u;
-                    const float r2 = u01(j0 ? w.a3 : w.b0);
-                    const int c2 = pick_of(r2);
-                    pick = c2;
-                    if (c2 <= nl) {
-                        const uint32_t q1 = j0 ? w.b0 : w.b1, q2 = j0 ? w.b1 : w.b2;
-                        u1 = u01(q1);
-                        u2 = u01(q2);
-                        gi_a = q1 >> 8;
-                        gi_b = q2 >> 8;
-                        gcos = c2 == nl;
-                        k += 3;
-                    } else {
-                        k += 1;
-                    }
-                }
             }
         };
         if (iter_lane) {
@@ -2645,6 +2642,8 @@ struct ipt_ctx {
     bool any_round_light = false;
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
     LightGrid lgrid;     // lgrid.pattern != 0: coplanar light lattice (kLightsGridA10/A01)
+    int sa_on = 0;       // the lights' sample points share the plane z = sa_pz, normal (0, 0, sa_nz) (skip-ahead)
+    float sa_pz = 0.0f, sa_nz = 0.0f;
     int* d_lgrid = nullptr;
     LightAx* d_lax = nullptr;  // lattice lights' compact records (IPT_LIGHT_AX_REC)
     int bpc_override = 0;
@@ -3150,6 +3149,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.lg_icw = ctx->lgrid.icw;
         kp.lg_ich = ctx->lgrid.ich;
         kp.lg_e = ctx->lgrid.e;
+        kp.sa_on = ctx->sa_on;
+        kp.sa_pz = ctx->sa_pz;
+        kp.sa_nz = ctx->sa_nz;
         kp.lg_pn = ctx->lgrid.pn;
         kp.lg_nn = ctx->lgrid.nn;
         kp.cos_a = ctx->d_cos_a;
@@ -3547,6 +3549,26 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->light_axis = (nl == 1 && !any_round && IPT_LIGHT_AXIS) ? axis_aligned_light(L[0]) : 0;
     if (ctx->light_axis && !(s->geometry_kind == IPT_GEOM_SPHERE_IN_BOX && light_ranges_box(L[0], 2, cam)))
         ctx->light_axis = 0;
+    // skip-ahead plane: one area light (or a lattice, whose lights share P.z
+    // and n.z bit for bit) whose axes have zero z components, so that every
+    // sampled point (x*u1 + y*u2) + P has z = P.z exactly, and whose normal is
+    // (+-0, +-0, n.z): a light sample's cosinus then has the sign of
+    // n.z * (o.z - P.z) whatever the draws (lighting.cpp:93-104, 125-134)
+    ctx->sa_on = 0;
+    {
+        auto zero = [](float f) { return (f2u(f) & 0x7fffffffu) == 0u; };
+        bool ok = nl >= 1 && !any_round && (nl == 1 || lg.pattern != 0);
+        for (int i = 0; ok && i < nl; ++i)
+            ok = (L[i].type == 0 || L[i].type == 1) && zero(L[i].x.z) && zero(L[i].y.z) && zero(L[i].n.x) &&
+                 zero(L[i].n.y) && !zero(L[i].n.z) && std::isfinite(L[i].n.z) && std::fabs(L[i].P.z) >= 0x1p-32f &&
+                 std::fabs(L[i].P.z) <= 0x1p32f &&
+                 f2u(L[i].P.z) == f2u(L[0].P.z) && f2u(L[i].n.z) == f2u(L[0].n.z);
+        if (ok) {
+            ctx->sa_on = 1;
+            ctx->sa_pz = L[0].P.z;
+            ctx->sa_nz = L[0].n.z;
+        }
+    }
     ctx->d_bvh_nodes = n_bvh_nodes.release();
     ctx->d_bvh_prims = n_bvh_prims.release();
     ctx->n_nodes = 0;
