@@ -405,7 +405,7 @@ def main():
         paths_launch = total_paths // world // args.steps
         path_alg_bytes = roofline.path_bytes(paths_launch, cos_samples // world // args.steps,
                                              cnt["sphere_frames"] // world // args.steps)
-        traffic = traffic_fabric = traffic_src = occ = dram = None
+        traffic = traffic_fabric = traffic_src = occ = dram = traffic_dram_upper = None
         for name in (f"pmc_latest_{args.config}.json",) + (("pmc_latest.json",) if args.config == "c2" else ()):
             pmc_file = ROOT / "profiles" / name
             if not pmc_file.exists():
@@ -415,11 +415,14 @@ def main():
                 c0 = pm.get("config", {})
                 if (c0.get("width") == W and c0.get("height") == H and c0.get("spp_per_step") == spp_step
                         and c0.get("depth_max", args.depth_max) == args.depth_max):
-                    # traffic: DRAM-destined bytes (TCC_EA0_RDREQ_DRAM / _WRREQ_DRAM share of
-                    # FETCH_SIZE / WRITE_SIZE); traffic_fabric: all L2 memory-side bytes
+                    # traffic: the measured L2 memory-side bytes (FETCH_SIZE + WRITE_SIZE,
+                    # MI355X_MICROARCH.md "HBM"); it counts Infinity-Cache hits too, so it
+                    # bounds the HBM bytes from above, as does the DRAM-destined request
+                    # estimate beside it (traffic_dram_upper)
                     traffic_fabric = pm.get("path_kernel_hbm_bytes_per_launch")
                     dram = pm.get("path_kernel_dram")
-                    traffic = pm.get("path_kernel_dram_bytes_per_launch", traffic_fabric)
+                    traffic = traffic_fabric
+                    traffic_dram_upper = pm.get("path_kernel_dram_bytes_per_launch")
                     occ = pm.get("path_kernel_occupancy")
                     cfg_tag = f"_{pm['config_name']}" if pm.get("config_name") else ""
                     traffic_src = (f"profiles/{pm['tag']}{cfg_tag}_summary.json (rocprofv3 --pmc passes of the same "
@@ -441,8 +444,10 @@ def main():
             "frac": hbm_ach / roofline.HBM_PEAK_GBPS,
             "traffic": traffic,
             "traffic_unit": "bytes/launch",
-            "traffic_kind": ("dram" if dram else "fabric") if traffic else None,
+            "traffic_kind": ("fabric: L2 memory-side bytes (FETCH_SIZE + WRITE_SIZE); Infinity-Cache hits "
+                             "included, so an upper bound on HBM bytes") if traffic else None,
             "traffic_fabric": traffic_fabric,
+            "traffic_dram_upper": traffic_dram_upper,
             "traffic_dram_detail": dram,
             "traffic_source": traffic_src,
             "measured_GBps": (traffic / launch_s / 1e9) if traffic else None,

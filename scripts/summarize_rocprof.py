@@ -84,7 +84,13 @@ if "TCC_EA0_RDREQ_sum" in pk and "TCC_EA0_RDREQ_DRAM_sum" in pk and "FETCH_SIZE"
     wr_share = 1.0
     if "TCC_EA0_WRREQ_sum" in pk and "TCC_EA0_WRREQ_DRAM_sum" in pk:
         wr_share = pk["TCC_EA0_WRREQ_DRAM_sum"] / max(pk["TCC_EA0_WRREQ_sum"], 1.0)
-    dram = (pk["FETCH_SIZE"] * rd_share + pk.get("WRITE_SIZE", 0.0) * wr_share) * 1024
+    # reads weighted by request size (64 B, or 32 B for the TCC_EA0_RDREQ_32B
+    # share, assumed the same among the DRAM-destined requests) rather than a
+    # request-count ratio applied to FETCH_SIZE; writes keep WRITE_SIZE's share
+    n32 = pk.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+    f32 = n32 / max(pk["TCC_EA0_RDREQ_sum"], 1.0)
+    rd_bytes = pk["TCC_EA0_RDREQ_DRAM_sum"] * (64.0 * (1.0 - f32) + 32.0 * f32)
+    dram = rd_bytes + pk.get("WRITE_SIZE", 0.0) * wr_share * 1024
     summary["path_kernel_dram_bytes_per_launch"] = dram
     summary["path_kernel_dram_bytes_per_path"] = dram / paths_per_launch
     summary["path_kernel_dram"] = {
@@ -92,8 +98,10 @@ if "TCC_EA0_RDREQ_sum" in pk and "TCC_EA0_RDREQ_DRAM_sum" in pk and "FETCH_SIZE"
         "read_dram_share": rd_share, "write_dram_share": wr_share,
         "read_requests_32B": pk.get("TCC_EA0_RDREQ_32B_sum"),
         "dram_credit_stall_cycles": pk.get("TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"),
-        "source": ("(FETCH_SIZE x RDREQ_DRAM/RDREQ + WRITE_SIZE x WRREQ_DRAM/WRREQ) x 1024; the Infinity "
-                   "Cache is memory-side, so DRAM-destined requests may include its hits (upper bound)"),
+        "read_32B_share": f32,
+        "source": ("RDREQ_DRAM x (64 B x (1 - 32B share) + 32 B x 32B share) + WRITE_SIZE x 1024 x WRREQ_DRAM/"
+                   "WRREQ; the Infinity Cache is memory-side, so DRAM-destined requests include its hits: an "
+                   "UPPER BOUND on HBM bytes (gfx950 tags every memory-side request DRAM-destined here)"),
     }
 if "SQ_WAVE_CYCLES" in pk and "GRBM_GUI_ACTIVE" in pk:
     busy = pk["GRBM_GUI_ACTIVE"] / N_XCD  # GPU-busy cycles of the dispatch
