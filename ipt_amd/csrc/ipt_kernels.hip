@@ -1988,9 +1988,18 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             bool has_li = false;
             vec3 li_pos = v3(0, 0, 0);
             float li_pow = 0.0f;
+            // coplanar lattice: the lights' shared n[2]*d[2] and plane quotient,
+            // computed once by the lookup below with light_trace_ax's operations
+            float lg_ndir = 0.0f, lg_t = 0.0f;
             auto light_step_with = [&](const LightDev& L, float wl) {
                 vec3 hp, hn;
-                const bool h = ltrace(L, ro, rd, &hp, &hn);
+                bool h;
+                if constexpr (grid_lights(LMODE) && IPT_LIGHT_INR) {
+                    constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
+                    h = light_trace_ax_t<XA, YA>(L, ro, rd, lg_ndir, lg_t, &hp, &hn);
+                } else {
+                    h = ltrace(L, ro, rd, &hp, &hn);
+                }
                 if (COUNT) ++c_ltest;
                 if (is_iter) lmix += wl * lpdf(L, ro, h, hp, hn);
                 if (h && (!has_li || longer(li_pos - ro, hp - ro))) {
@@ -2039,8 +2048,14 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 // <= 4 cells, in index order, are the scan's hits (a light that
                 // is not hit adds +0 to lmix and is never nearest)
                 constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
+                // (the lattice's ranges are proven like the single light's,
+                // light_ranges_box: the range-free quotient of light_trace_ax,
+                // shared with the light tests below)
                 const float n_dir = kp.lg_nn * comp<2>(rd);
-                const float t = div_(kp.lg_nn * (kp.lg_pn - comp<2>(ro)), n_dir);
+                const float num = kp.lg_nn * (kp.lg_pn - comp<2>(ro));
+                const float t = IPT_LIGHT_INR ? div_inrange_(num, n_dir) : div_(num, n_dir);
+                lg_ndir = n_dir;
+                lg_t = t;
                 const float u = (comp<XA>(ro) + comp<XA>(rd) * t - kp.lg_u0) * kp.lg_icw;
                 const float v = (comp<YA>(ro) + comp<YA>(rd) * t - kp.lg_v0) * kp.lg_ich;
                 int cand[4] = {-1, -1, -1, -1};
