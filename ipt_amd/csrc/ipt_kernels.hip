@@ -1547,7 +1547,22 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     // <= that start <= r, so the scan would pass it; a bucket holds
                     // at most 8 entries (else the table is not built)
                     c = cdf_lo_lds[(int)(r * 256.0f)];
-                    while (c <= nl && !(r < LS.cdf(c))) ++c;
+                    if (kp.cdf_bsearch) {
+                        // non-decreasing cdf: the answer is c plus the number of
+                        // the entries from c on that r does not undercut, a
+                        // prefix; the first three are read at once (C5: two
+                        // lights per bucket), the scan past them is a rare branch
+                        const float f0 = LS.cdf(min(c, nl)), f1 = LS.cdf(min(c + 1, nl)), f2 = LS.cdf(min(c + 2, nl));
+                        const int n0 = (c <= nl && !(r < f0)) ? 1 : 0;
+                        const int n1 = (c + 1 <= nl && !(r < f1)) ? 1 : 0;
+                        const int n2 = (c + 2 <= nl && !(r < f2)) ? 1 : 0;
+                        const bool more = n2 != 0;
+                        c += n0 + n1 + n2;
+                        if (__builtin_expect(__any(more), 0))
+                            if (more) while (c <= nl && !(r < LS.cdf(c))) ++c;
+                    } else {
+                        while (c <= nl && !(r < LS.cdf(c))) ++c;
+                    }
                 } else if ((global_lights(LMODE) || LMODE == kLightsAny) && kp.cdf_bsearch) {
                     // first c with r < cdf[c] (else nl+1): the scan's answer on a
                     // non-decreasing cdf (checked at upload)
