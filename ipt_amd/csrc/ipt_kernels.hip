@@ -2006,12 +2006,13 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             // coplanar lattice: the lights' shared n[2]*d[2] and plane quotient,
             // computed once by the lookup below with light_trace_ax's operations
             float lg_ndir = 0.0f, lg_t = 0.0f;
+            vec3 lg_q = v3(0, 0, 0);
             auto light_step_with = [&](const LightDev& L, float wl) {
                 vec3 hp, hn;
                 bool h;
                 if constexpr (grid_lights(LMODE) && IPT_LIGHT_INR) {
                     constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
-                    h = light_trace_ax_t<XA, YA>(L, ro, rd, lg_ndir, lg_t, &hp, &hn);
+                    h = light_trace_ax_q<XA, YA>(L, lg_ndir, lg_t, lg_q, &hp, &hn);
                 } else {
                     h = ltrace(L, ro, rd, &hp, &hn);
                 }
@@ -2071,8 +2072,9 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 const float t = IPT_LIGHT_INR ? div_inrange_(num, n_dir) : div_(num, n_dir);
                 lg_ndir = n_dir;
                 lg_t = t;
-                const float u = (comp<XA>(ro) + comp<XA>(rd) * t - kp.lg_u0) * kp.lg_icw;
-                const float v = (comp<YA>(ro) + comp<YA>(rd) * t - kp.lg_v0) * kp.lg_ich;
+                lg_q = ro + rd * t;
+                const float u = (comp<XA>(lg_q) - kp.lg_u0) * kp.lg_icw;
+                const float v = (comp<YA>(lg_q) - kp.lg_v0) * kp.lg_ich;
                 int cand[4] = {-1, -1, -1, -1};
                 const float e = kp.lg_e;
                 if (u > -1.0f && u < (float)kp.lg_nu + 1.0f && v > -1.0f && v < (float)kp.lg_nv + 1.0f) {

@@ -415,11 +415,11 @@ IPT_HD float comp(vec3 v) {
 // sqrt_inrange_: bit-identical in range, ipt_math.h). Where a quotient is out
 // of range its result is never observed (the hit is rejected or the lane's
 // pdf is not used), exactly as its IEEE value would not be.
-// (light_trace_ax_t: the same test from the light's n_dir and t, which every
-// light of a coplanar lattice shares -- the lattice lookup computes them once
-// with these operations)
+// (light_trace_ax_q: the same test from the light's n_dir, t and plane point
+// q = o + d*t, which every light of a coplanar lattice shares -- the lattice
+// lookup computes them once with these operations)
 template <int XA, int YA>
-IPT_HD bool light_trace_ax_t(const LightDev& L, vec3 o, vec3 d, float n_dir, float t, vec3* hit, vec3* nrm);
+IPT_HD bool light_trace_ax_q(const LightDev& L, float n_dir, float t, vec3 q, vec3* hit, vec3* nrm);
 template <int XA, int YA, bool INR = false>
 IPT_HD bool light_trace_ax(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* nrm) {
     constexpr int NA = 3 - XA - YA;
@@ -427,11 +427,11 @@ IPT_HD bool light_trace_ax(const LightDev& L, vec3 o, vec3 d, vec3* hit, vec3* n
     // INR: |num| is 0 or in [2^-40, 2^41); |n_dir| >= 1e-6 wherever t is used
     const float num = comp<NA>(L.n) * (comp<NA>(L.P) - comp<NA>(o));
     const float t = INR ? div_inrange_(num, n_dir) : div_(num, n_dir);
-    return light_trace_ax_t<XA, YA>(L, o, d, n_dir, t, hit, nrm);
+    return light_trace_ax_q<XA, YA>(L, n_dir, t, o + d * t, hit, nrm);
 }
 template <int XA, int YA>
-IPT_HD bool light_trace_ax_t(const LightDev& L, vec3 o, vec3 d, float n_dir, float t, vec3* hit, vec3* nrm) {
-    const vec3 rel = (o + d * t) - L.P;
+IPT_HD bool light_trace_ax_q(const LightDev& L, float n_dir, float t, vec3 q, vec3* hit, vec3* nrm) {
+    const vec3 rel = q - L.P;
     const float cx = comp<0>(L.inv.c[XA]) * comp<XA>(rel);
     const float cy = comp<1>(L.inv.c[YA]) * comp<YA>(rel);
     const bool in = L.type == 0 ? (cx >= 0.0f) & (cx <= 1.0f) & (cy >= 0.0f) & (cy <= 1.0f)
