@@ -307,7 +307,13 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
          z = x; the self-check compares the path kernel's frame table
       16 (ipt_math_selfcheck only) the sphere-in-box frame without glm's
          zero terms against the exact build, over directions hashed from
-         the bit pattern (incl. zero / tiny x and y) */
+         the bit pattern (incl. zero / tiny x and y)
+      17 / 18 (ipt_math_selfcheck only) the reciprocal by the hardware rcp
+         and one / two Newton corrections against the round-4 range-free
+         1.0f / x sequence (three corrections)
+      19 / 20 (ipt_math_selfcheck only) the range-free division against
+         IEEE a/b over the division pairs of 10 / pairs whose divisors have
+         all-ones-like significands */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 /* Philox4x32-10 blocks exactly as the kernels generate the per-path stream
    that replaces randf() (include/randf.h:6-11; draw k of path (pass s, pixel

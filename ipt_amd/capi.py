@@ -372,6 +372,9 @@ MATH_FNS = {"acosf": 0, "sinf": 1, "cosf": 2, "acos_f64_f32": 3, "sincosf_sin": 
             "div_inrange_pairs": 10, "longer_pairs": 11, "udiv_exact_pairs": 12,
             "sqrt_inrange": 13, "frame_angle_sin": 14, "frame_angle_cos": 15}
 SELFCHECK_FRAME_FAST = 16  # ipt_math_selfcheck only: fast vs exact sphere-in-box frame
+# ipt_math_selfcheck only: reciprocal with 1 / 2 Newton corrections vs the round-4 three-correction
+# sequence; the range-free division vs IEEE over the division pairs / near-all-ones divisors
+SELFCHECK_RCP1, SELFCHECK_RCP2, SELFCHECK_DIV_PAIRS, SELFCHECK_DIV_ONES = 17, 18, 19, 20
 
 
 def shard_plan(p: Params):

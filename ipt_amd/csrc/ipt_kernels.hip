@@ -2361,6 +2361,15 @@ __device__ __host__ inline float div_pair_b(uint32_t b) {
     return u2f((h & 0x807fffffu) | ((87u + ((h >> 23) & 0xffu) % 81u) << 23));
 }
 
+// fn 20: divisors whose significands are all ones or within 2^12 ulps of it
+// (the hard case of one-correction division), hashed exponents as above
+__device__ __host__ inline float div_pair_b_ones(uint32_t b) {
+    uint32_t h = b * 0x85EBCA77u;
+    h ^= h >> 13;
+    const uint32_t m = 0x007fffffu - (h & 0xfffu);
+    return u2f((h & 0x80000000u) | ((87u + ((h >> 12) & 0xffu) % 81u) << 23) | m);
+}
+
 // fn 11 / 12 probes: a 32-bit pattern b seeds a pair.
 //  11: x = |b| as a float, y = x moved by a hashed -64..63 ulps (every 16th
 //      pair: an unrelated hashed float) -> longer_sq(x, y) as 0/1;
@@ -2406,6 +2415,10 @@ __device__ __host__ inline float math_fn(int fn, float x) {
             frame_angle_sc(v3(0.6f, 0.8f, x), &sv, &cv);
             return fn == 14 ? sv : cv;
         }
+        case 17: return rcp_newton_<1>(x);
+        case 18: return rcp_newton_<2>(x);
+        case 19: return div_inrange_(div_pair_a(f2u(x)), div_pair_b(f2u(x)));
+        case 20: return div_inrange_(div_pair_a(f2u(x)), div_pair_b_ones(f2u(x)));
         case 0: return acosf_(x);
         case 1: return sinf_(x);
         case 2: return cosf_(x);
@@ -2533,6 +2546,14 @@ __device__ float math_fn_exact(int fn, float x) {
     }
     if (fn == 12) return u2f(f2u(x) / udiv_pair_d(f2u(x)));
     if (fn == 13) return __builtin_sqrtf(x);  // IEEE (compiler sequence)
+    if (fn == 17 || fn == 18) {  // the round-4 reciprocal: one Newton step, two quotient residual steps
+        float y = __builtin_amdgcn_rcpf(x);
+        y = __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
+        const float q1 = __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
+        return __builtin_fmaf(__builtin_fmaf(-x, q1, 1.0f), y, q1);
+    }
+    if (fn == 19) return div_pair_a(f2u(x)) / div_pair_b(f2u(x));       // IEEE (compiler sequence)
+    if (fn == 20) return div_pair_a(f2u(x)) / div_pair_b_ones(f2u(x));  // IEEE (compiler sequence)
     return math_fn(fn, x);
 }
 
@@ -2593,8 +2614,8 @@ __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long lo
             frame_sc_lookup(ftab, v3(0.6f, 0.8f, x), sv, cv);
             a = fn == 14 ? sv : cv;
         }
-        // fn 10: a zero quotient's sign is not observed by the callers
-        if (!(f2u(a) == f2u(e) || (a != a && e != e) || (fn == 10 && a == 0.0f && e == 0.0f))) {
+        // fn 10 / 19 / 20: a zero quotient's sign is not observed by the callers
+        if (!(f2u(a) == f2u(e) || (a != a && e != e) || ((fn == 10 || fn >= 19) && a == 0.0f && e == 0.0f))) {
             ++local;
             atomicMin(first, b);
         }
@@ -3854,7 +3875,7 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
                        uint32_t* first_bad) {
-    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 16 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 20 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
         return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     if (fn == 14 || fn == 15) {

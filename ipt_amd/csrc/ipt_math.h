@@ -55,22 +55,47 @@ IPT_HD float sqrt_(float x) { return __builtin_sqrtf(x); }
 IPT_HD float div_(float a, float b) { return a / b; }
 
 // a/b without the range handling of the compiler's sequence (no v_div_scale /
-// v_div_fmas / v_div_fixup): the reciprocal, one Newton step and two quotient
-// residual steps. Bit-identical to a/b when |a| in [2^-40, 2^41) or a = +-0
-// (then a signed zero, whose sign the callers never observe) and |b| in
-// [2^-40, 2^41): the device proof is ipt_math_selfcheck fn 9 (2^32 pairs).
-// Callers must guarantee the range.
+// v_div_fmas / v_div_fixup): the reciprocal, one Newton step and ONE quotient
+// residual step (round 5; two before). Bit-identical to a/b when |a| in
+// [2^-40, 2^41) or a = +-0 (then a signed zero, whose sign the callers never
+// observe) and |b| in [2^-40, 2^41). Why one residual step suffices: the
+// Newton step makes y = RN(1/b) (exhaustively, fn 17 below), and with y the
+// correctly rounded reciprocal and q0 = RN(a*y) within an ulp of a/b, q0 +
+// y*RN(a - b*q0) (the residual exact by fma) is the correctly rounded quotient
+// in the absence of over/underflow (Markstein's theorem for fma division).
+// Device checks: ipt_math_selfcheck fn 10 (2^32 hashed pairs over the range)
+// and fn 20 (2^32 pairs with divisors of all-ones-like significands, the
+// theorem's hard case), 0 mismatches. Callers must guarantee the range.
 IPT_HD float div_inrange_(float a, float b) {
 #if defined(__HIP_DEVICE_COMPILE__)
     float y = __builtin_amdgcn_rcpf(b);
     y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
     const float q0 = a * y;
-    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
-    return __builtin_fmaf(__builtin_fmaf(-b, q1, a), y, q1);
+    return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
 #else
     return a / b;
 #endif
 }
+
+// 1/b by the hardware reciprocal and Newton corrections: STEPS = 1 (y1) or 2
+// (y2) of the corrections that the round-4 div_inrange_(1.0f, b) applied (y1,
+// then q1 == y2, then q2). ipt_math_selfcheck fn 17 / 18 compare them with
+// that three-correction sequence over all 2^32 floats: both are identical to
+// it bit for bit everywhere (round 5, `profiles/round5_rcp_check.txt`), so
+// rcp_inrange_ below takes one correction instead of three.
+template <int STEPS>
+IPT_HD float rcp_newton_(float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float y = __builtin_amdgcn_rcpf(b);
+    y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+    if (STEPS >= 2) y = __builtin_fmaf(__builtin_fmaf(-b, y, 1.0f), y, y);
+    return y;
+#else
+    return 1.0f / b;
+#endif
+}
+// == the three-correction 1.0f / b for every float b (exhaustive device check above)
+IPT_HD float rcp_inrange_(float b) { return rcp_newton_<1>(b); }
 
 // Correctly rounded sqrtf for x = +0 or in [2^-96, 2^126): the hardware root (within
 // one ulp, no denormal scaling needed in this range) corrected by the signs of
@@ -121,7 +146,7 @@ IPT_HD vec3 normalize(vec3 v) {
 // normalize for dot(v, v) in [2^-80, 2^80] (root in [2^-40, 2^40]): the same
 // roundings as normalize() through the range-free root and quotient
 IPT_HD vec3 normalize_inrange_(vec3 v) {
-    const float s = div_inrange_(1.0f, sqrt_inrange_(dot(v, v)));
+    const float s = rcp_inrange_(sqrt_inrange_(dot(v, v)));
     return v * s;
 }
 
@@ -149,7 +174,7 @@ IPT_HD mat3 inverse(const mat3& M) {
     det = det - m10 * (m01 * m22 - m21 * m02);
     det = det + m20 * (m01 * m12 - m11 * m02);
     // glm writes "+ m00*(..) - m10*(..) + m20*(..)"; unary + is exact
-    const float o = INRANGE ? div_inrange_(1.0f, det) : div_(1.0f, det);  // INRANGE: det in [2^-40, 2^41)
+    const float o = INRANGE ? rcp_inrange_(det) : div_(1.0f, det);  // INRANGE: det in [2^-40, 2^41)
     mat3 I;
     I.c[0].x = (m11 * m22 - m21 * m12) * o;
     I.c[1].x = -(m10 * m22 - m20 * m12) * o;

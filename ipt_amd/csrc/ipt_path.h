@@ -63,7 +63,7 @@ IPT_HD Frame make_frame_sc(vec3 to, float s, float c) {
         const float r = sqrt_inrange_(q);
         const bool rep = (q < 0x1p-80f) | lt_1em6(r);
         axis = rep ? v3(1.0f, 0.0f, 0.0f) : axis;
-        ax = axis * div_inrange_(1.0f, rep ? 1.0f : r);
+        ax = axis * rcp_inrange_(rep ? 1.0f : r);
     } else {
         if (lt_1em6(length(axis))) axis = v3(1.0f, 0.0f, 0.0f);
         ax = normalize(axis);
@@ -107,7 +107,7 @@ IPT_HD Frame make_frame_sc_fast(vec3 to, float s, float c, bool& ok) {
     const float axx = -to.y, axy = to.x;  // cross((0,0,1), to).xy when non-zero
     const float q = axx * axx + axy * axy;
     const float r = sqrt_inrange_(q);
-    const float inv = div_inrange_(1.0f, r);
+    const float inv = rcp_inrange_(r);
     const float ax = axx * inv, ay = axy * inv;
     const float omc = 1.0f - c;
     const float tx = omc * ax, ty = omc * ay;
@@ -448,7 +448,7 @@ IPT_HD float light_pdf_ax(const LightDev& L, vec3 o, bool has, vec3 hit, vec3 nr
     const vec3 ho = hit - o;
     const float decay = dot(ho, ho);
     // INR on a hit: decay in [dmin^2, dmax^2], cosinus in [~1e-6, 1], area in range
-    const float s = INR ? div_inrange_(1.0f, sqrt_inrange_(decay))
+    const float s = INR ? rcp_inrange_(sqrt_inrange_(decay))
                         : div_(1.0f, sqrt_(decay));  // normalize's 1/sqrt(dot(v,v)) (same dot)
     const float cosinus = comp<NA>(nrm) * -(comp<NA>(ho) * s);
     const float p = INR ? div_inrange_(div_inrange_(decay, cosinus), L.area) : div_(div_(decay, cosinus), L.area);

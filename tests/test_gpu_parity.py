@@ -157,6 +157,18 @@ def test_fast_math_exhaustive(gpu_ctx, fn):
     assert bad == 0, (fn, bad, hex(first))
 
 
+@pytest.mark.parametrize("fn", ["SELFCHECK_RCP1", "SELFCHECK_RCP2", "SELFCHECK_DIV_PAIRS", "SELFCHECK_DIV_ONES"])
+def test_short_division_exhaustive(gpu_ctx, fn):
+    """The round-5 range-free reciprocal (the hardware rcp and one Newton
+    correction) equals the round-4 three-correction sequence on all 2^32
+    floats (17; 18: two corrections), and the range-free division with one
+    quotient residual step equals IEEE a/b on 2^32 hashed pairs over its range
+    (19) and on 2^32 pairs whose divisors have all-ones-like significands
+    (20, the hard case of Markstein's one-step theorem)."""
+    bad, first = gpu_ctx.math_selfcheck(getattr(capi, fn))
+    assert bad == 0, (fn, bad, hex(first))
+
+
 def test_fast_frame_matches_exact(gpu_ctx):
     """The sphere-in-box frame without glm's zero terms (make_frame_sc_fast)
     equals the exact RotateDdf build (make_frame_sc<true>) bit for bit on every
