@@ -14,7 +14,6 @@
 #   profile=CFG,CFG       rocprof stats + PMC traffic passes + bench lines (TAG env)
 #   phases=CFG,CFG        IPT_PROF / IPT_STAMP builds' phase profiles (scripts/prof_phases.sh first)
 #   ubench                VALU / packed-f32 issue microbenchmark (scripts/ubench_valu)
-#   pcsamp                rocprofv3 PC sampling of one C2 step (if the box allows it)
 #
 # usage (gpurun): /usr/local/graft/bin/gpurun --timeout 900 -- 'bash scripts/gpu_job.sh tests=async bench=c2'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -73,13 +72,6 @@ step() {
       CONFIGS="${v//,/ }" bash scripts/gpu_prof_phases.sh ;;
     ubench)
       timeout -k 10 300 ./scripts/ubench_valu > gpurun_out/ubench_valu.jsonl && cat gpurun_out/ubench_valu.jsonl ;;
-    pcsamp)
-      timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method "${METHOD:-host_trap}" \
-        --pc-sampling-unit "${UNIT:-time}" --pc-sampling-interval "${INTERVAL:-1}" --output-format csv \
-        -d gpurun_out/pcs -o pcs -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 --no-counters --sync \
-        > gpurun_out/pcs_bench.json 2> gpurun_out/pcs.err; local rc=$?
-      tail -3 gpurun_out/pcs.err; find gpurun_out/pcs -type f | head -5
-      return $rc ;;
     *) echo "unknown step $s"; return 2 ;;
   esac
 }
