@@ -103,6 +103,9 @@ struct KParams {
     // with sa_nz * (sa_pz - z) >= 0 are certain skips (sa_on, host-checked)
     int sa_on;
     float sa_pz, sa_nz;
+    // a pick r < sa_cl is a light pick (one light: cdf[0]; a lattice with a
+    // non-decreasing cdf: cdf[nl - 1]; else 0, never)
+    float sa_cl;
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
@@ -1309,6 +1312,9 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
     // certain light-sample skips taken within the step (the prologue below):
     // the axis-aligned single-light instances, whose ranges are proven
     constexpr bool kSkipAhead = IPT_SKIP_AHEAD && (one_light(LMODE) || grid_lights(LMODE)) && !kResL;
+    // ... and the next iteration's certain skip taken at the end of the step,
+    // before its pop (the instances that pop at the end of the step)
+    constexpr bool kPreSkip = kSkipAhead && IPT_PRE_SKIP && kFramePf == 3;
     bool tracing = false;  // a resumable walk (sphere list or light BVH) is in progress
     float xlmix = 0.0f;    // light walk: the running UnionDdf light sum
     vec3 xro = v3(0, 0, 0), xrd = v3(0, 0, 0), xli_pos = v3(0, 0, 0);
@@ -1468,6 +1474,10 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
         // path and the compiler's waits drain only what they wait for
         uint32_t gi_a = 0, gi_b = 0;
         bool gcos = false;
+        // kPreSkip: the word after the iteration's draws (the next pick) and
+        // whether the end of the step may take it (set by the prologue)
+        uint32_t pre_w = 0u;
+        bool pre_ok = false;
         // IPT_LPF (lattice instances): the picked light's sample fields are
         // gathered with the CosineDdf gathers (whole wave, index 0 for lanes
         // without a light pick) instead of read in the direction phase
@@ -1534,8 +1544,11 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 philox_fill(w.b0, w.b1, w.b2, w.b3, blk + 1, rpass, rpix, kp.key0, kp.key1);
                 need_b = false;
             }
-            const uint32_t j = k & 3u;  // = k - 4*blk: the window was shifted above
-            const float r = u01(sel4(j, w.a0, w.a1, w.a2, w.a3));
+            // j = k - 4*blk: the window was shifted above. kPreSkip: a step that
+            // took the next pick's skip may end 9 words past blk, so after the
+            // one shift j <= 5 (words j .. j+2 are still in the window)
+            const uint32_t j = kPreSkip ? k - 4u * blk : k & 3u;
+            const float r = u01(kPreSkip && j >= 4u ? (j & 1u ? w.b1 : w.b0) : sel4(j & 3u, w.a0, w.a1, w.a2, w.a3));
             // UnionDdf::sample's component: the first c with r < cdf[c] (ddf.cpp:142-153)
             auto pick_of = [&](float r) {
                 int c = 0;
@@ -1614,10 +1627,17 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             }
             pick = c;
             if (c <= nl) {
-                // words jj+1, jj+2 (jj <= 4 in the skip-ahead instances, else <= 3)
-                const bool hi = kSkipAhead && jj == 4u;
-                const uint32_t r1 = hi ? w.b1 : sel4(jj & 3u, w.a1, w.a2, w.a3, w.b0);
-                const uint32_t r2 = hi ? w.b2 : sel4(jj & 3u, w.a2, w.a3, w.b0, w.b1);
+                // words jj+1, jj+2 (jj <= 4 in the skip-ahead instances, <= 5
+                // with kPreSkip, else <= 3)
+                const bool hi = kSkipAhead && jj >= 4u;
+                const uint32_t r1 = hi ? (kPreSkip && (jj & 1u) ? w.b2 : w.b1) : sel4(jj & 3u, w.a1, w.a2, w.a3, w.b0);
+                const uint32_t r2 = hi ? (kPreSkip && (jj & 1u) ? w.b3 : w.b2) : sel4(jj & 3u, w.a2, w.a3, w.b0, w.b1);
+                if constexpr (kPreSkip) {
+                    // the next pick's word jj+3 (taken only at jj <= 3: the step
+                    // then ends at most 9 words past blk)
+                    pre_w = sel4(jj & 3u, w.a3, w.b0, w.b1, w.b2);
+                    pre_ok = jj <= 3u && kp.sa_on;
+                }
                 u1 = u01(r1);
                 u2 = u01(r2);
                 if (c == nl) {
@@ -2217,6 +2237,27 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             }
         }
         }  // !kResL
+        if constexpr (kPreSkip) {
+            // The next iteration of the lane's node -- the same node's next one,
+            // or the first of the child pushed in this step -- is a certain skip
+            // when its pick word (read by the prologue: word jj+3) picks a light
+            // and the node lies behind the lights' plane (the prologue's
+            // skip-ahead argument). It does nothing but consume its three draws
+            // and count (main.cpp:149-163), so it is taken here: a node whose
+            // last iteration it was is then done and popped below in this step
+            // (instead of a step of its own for the skip). Same draws in the
+            // same order, same counts.
+            // (as selects: no exec-mask branch)
+            const bool back = (tpos.z - kp.sa_pz) * kp.sa_nz < 0.0f;
+            const bool take = iter_lane && pre_ok && back && ti < (kp.n_rays >> tdepth) && u01(pre_w) < kp.sa_cl;
+            ti += take ? 1 : 0;
+            k += take ? 3u : 0u;
+            if (COUNT) {
+                c_iter += take ? 1u : 0u;
+                c_lsamp += take ? 1u : 0u;
+                c_skip += take ? 1u : 0u;
+            }
+        }
         if constexpr (kFramePf == 3) {
             pop_node();
             IPT_STAMP_AT(6);  // pop (end of step)
@@ -2696,7 +2737,7 @@ struct ipt_ctx {
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
     LightGrid lgrid;     // lgrid.pattern != 0: coplanar light lattice (kLightsGridA10/A01)
     int sa_on = 0;       // the lights' sample points share the plane z = sa_pz, normal (0, 0, sa_nz) (skip-ahead)
-    float sa_pz = 0.0f, sa_nz = 0.0f;
+    float sa_pz = 0.0f, sa_nz = 0.0f, sa_cl = 0.0f;
     int* d_lgrid = nullptr;
     LightAx* d_lax = nullptr;  // lattice lights' compact records (IPT_LIGHT_AX_REC)
     int bpc_override = 0;
@@ -3205,6 +3246,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.sa_on = ctx->sa_on;
         kp.sa_pz = ctx->sa_pz;
         kp.sa_nz = ctx->sa_nz;
+        kp.sa_cl = ctx->sa_cl;
         kp.lg_pn = ctx->lgrid.pn;
         kp.lg_nn = ctx->lgrid.nn;
         kp.cos_a = ctx->d_cos_a;
@@ -3620,6 +3662,9 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
             ctx->sa_on = 1;
             ctx->sa_pz = L[0].P.z;
             ctx->sa_nz = L[0].n.z;
+            // UnionDdf::sample picks a light (c < nl) iff r < cdf[c] for some
+            // c < nl, i.e. iff r < cdf[nl - 1] on a non-decreasing cdf
+            ctx->sa_cl = (nl == 1 || cdf_mono) ? cdf[nl - 1] : 0.0f;
         }
     }
     ctx->d_bvh_nodes = n_bvh_nodes.release();

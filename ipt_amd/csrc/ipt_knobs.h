@@ -14,7 +14,7 @@
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG) || \
-     defined(IPT_COSB_TAB) || defined(IPT_SKIP_AHEAD))
+     defined(IPT_COSB_TAB) || defined(IPT_SKIP_AHEAD) || defined(IPT_PRE_SKIP))
 #error "an ipt_knobs.h parameter is overridden: A/B builds must define IPT_AB_BUILD"
 #endif
 
@@ -71,6 +71,10 @@
 #endif
 #ifndef IPT_SKIP_AHEAD
 #define IPT_SKIP_AHEAD 1  // single axis-aligned light: a certain light-sample skip and the next pick in one step
+#endif
+#ifndef IPT_PRE_SKIP
+#define IPT_PRE_SKIP 1  // skip-ahead instances with the end-of-step pop: the next iteration's certain skip
+                        // taken at the end of the step (before the pop)
 #endif
 #ifndef IPT_COSB_TAB
 #define IPT_COSB_TAB 0  // non-resumable instances: CosineDdf's (cos phi, sin phi) gathered from the 128 MiB table

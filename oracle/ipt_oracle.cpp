@@ -561,6 +561,9 @@ float ray_power(const Ctx& cx, V3 origin, V3 direction, int depth, int n_rays) {
     float res = 0.0f;
     for (int i = 0; i < n_rays; ++i) {
         if (g_cnt) ++g_cnt->iters;
+#ifdef IPT_ORACLE_ITER_HOOK
+        const uint32_t k_at = g_rng ? g_rng->k : 0u;  // analysis builds only (scripts/skip_stats.cpp)
+#endif
         // UnionDdf::sample (ddf.cpp:139-154)
         V3 new_direction = mk(0, 0, 0);  // fall-through (sum of weights < 1): defined as vec3()
         float r = randf();
@@ -583,6 +586,9 @@ float ray_power(const Ctx& cx, V3 origin, V3 direction, int depth, int n_rays) {
                 break;
             }
         }
+#ifdef IPT_ORACLE_ITER_HOOK
+        IPT_ORACLE_ITER_HOOK(depth, i, n_rays, k_at, new_direction == mk(0, 0, 0), si.position);
+#endif
         if (new_direction == mk(0, 0, 0)) {
             if (g_cnt) ++g_cnt->skipped;
             continue;
