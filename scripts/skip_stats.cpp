@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     Ctx cx{&sc, &mix, p.depth_max};
     // policies: steps per path when certain skips merge into the next iteration's step
     uint64_t paths = 0, iters = 0, skips = 0, cert = 0, cert_last = 0, cert_j[4] = {}, cert_chain = 0,
-             n1_cert = 0, merged_cur = 0, merged_any1 = 0, merged_chain = 0, sim_steps[kPol] = {}, sim_bad[kPol] = {};
+             n1_cert = 0, merged_cur = 0, merged_any1 = 0, merged_chain = 0, sim_steps[kPol] = {}, sim_bad[kPol] = {}, rem[4] = {}, rem_j[6] = {};
     std::vector<Ev> evs;
     g_evs = &evs;
     for (int s = 0; s < spp; ++s)
@@ -106,6 +106,16 @@ int main(int argc, char** argv) {
                             const Ev& b = evs[nx];
                             if (b.skip && b.back && b.i != b.n - 1 && b.k - 4u * blk <= q.omax) ++nx;
                         }
+                        if (pol == 3) {
+                            // the step's own event when it is still a certain skip (a lane-step spent on it)
+                            const Ev& a = evs[r];
+                            if (a.skip && a.back) {
+                                const bool after_pop = r > 0 && evs[r - 1].depth > a.depth;
+                                const bool last = a.i == a.n - 1;
+                                ++rem[(after_pop ? 2 : 0) + (last ? 1 : 0)];
+                                if (!after_pop && !last) ++rem_j[j > 5u ? 5u : j];
+                            }
+                        }
                         e = nx;
                     }
                 }
@@ -137,6 +147,10 @@ int main(int argc, char** argv) {
     for (int pol = 0; pol < kPol; ++pol)
         std::printf("%-55s lane-steps per path %.3f (j beyond the window: %llu)\n", kPols[pol].name,
                     sim_steps[pol] / P, (unsigned long long)sim_bad[pol]);
+    std::printf("product policy: certain-skip lane-steps left: not after a pop: non-last %.3f last %.3f | after a pop: non-last %.3f last %.3f\n",
+                rem[0] / P, rem[1] / P, rem[2] / P, rem[3] / P);
+    std::printf("  (not after a pop, non-last, by j: %.3f %.3f %.3f %.3f %.3f %.3f)\n", rem_j[0] / P, rem_j[1] / P,
+                rem_j[2] / P, rem_j[3] / P, rem_j[4] / P, rem_j[5] / P);
     std::printf("paths %llu iterations/path %.3f skipped %.3f certain %.3f (last-iteration %.3f, n=1 nodes %.3f)\n",
                 (unsigned long long)paths, iters / P, skips / P, cert / P, cert_last / P, n1_cert / P);
     std::printf("certain by window offset j: %.3f %.3f %.3f %.3f; second-in-a-row %.3f\n", cert_j[0] / P,
