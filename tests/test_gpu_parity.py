@@ -70,6 +70,30 @@ def test_counters_match_oracle(gpu_ctx, oracle):
         assert g[k] == o[k], (k, g[k], o[k])
 
 
+@pytest.mark.parametrize("name", ["box_lights16", "box_lights256", "random64", "lit_corner", "square", "spheres300"])
+def test_counters_match_oracle_scenes(gpu_ctx, oracle, name):
+    """The oracle's event counts in the other instances: the single-light and
+    lattice instances that take certain skips ahead in the prologue and at the
+    end of the step (skip-ahead, pre-skip), and the generic ones that do not.
+    Every skipped iteration must be counted as the reference counts it."""
+    desc = {"box_lights16": lambda: scenes.make_scene_box_lights(4),
+            "box_lights256": lambda: scenes.make_scene_box_lights(16),
+            "random64": lambda: scenes.make_scene_random_lights(64),
+            "lit_corner": scenes.make_scene_lit_corner,
+            "square": scenes.make_scene_square_lit_by_square,
+            "spheres300": lambda: scenes.make_scene_spheres(300)}[name]()
+    W, H = 24, 20
+    gpu_ctx.upload_scene(desc)
+    gpu_ctx.reset_counters()
+    vals, codes = gpu_ctx.render_values(capi.make_params(W, H, 2, flags=capi.IPT_FLAG_COUNTERS))
+    g = gpu_ctx.counters()
+    ov, oc, o = ob.render_values(desc, capi.make_params(W, H, 2), 0, with_counters=True)
+    assert np.array_equal(_bits(vals), _bits(ov))
+    for k in ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
+              "iterations", "light_samples", "skipped", "drifted"):
+        assert g[k] == o[k], (name, k, g[k], o[k])
+
+
 @pytest.mark.parametrize("fn", sorted(capi.MATH_FNS.values()))
 def test_device_math_matches_host(gpu_ctx, fn):
     """Device build of ipt_math.h == host build (which equals glibc, see
