@@ -108,6 +108,11 @@ struct KParams {
     float sa_cl;
     float lg_pn, lg_nn;                   // the lights' shared plane: P[na], n[na]
     int cdf_bsearch;                      // cdf non-decreasing: pick by binary search
+    // |cdf[i] - (i+1) 2^-e| < 2^-e/2 for every light i and a non-decreasing
+    // cdf (host-checked): the pick is floor(r 2^e) - 1, + 0 or + 1 by two cdf
+    // entries, then cdf[nl] decides past the lights (cdf_p2s = 2^e)
+    int cdf_p2;
+    float cdf_p2s, cdf_end;
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
@@ -1554,6 +1559,12 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 int c = 0;
                 if (one_light(LMODE)) {
                     c = r < LS.c0 ? 0 : (r < LS.c1 ? 1 : 2);
+                } else if (global_lights(LMODE) && IPT_CDF_POW2 && kp.cdf_p2) {
+                    // (host-checked near-uniform cdf: ce - 1, ce or ce + 1)
+                    const int ce = min((int)(r * kp.cdf_p2s), nl);
+                    const float fa = LS.cdf(max(ce - 1, 0)), fb = LS.cdf(ce);
+                    c = (ce >= 1 && r < fa) ? ce - 1 : (r < fb ? ce : ce + 1);
+                    if (c >= nl) c = r < kp.cdf_end ? nl : nl + 1;
                 } else if (global_lights(LMODE) && kp.cdf_lo) {
                     // the scan from the first index whose cdf exceeds r's bucket
                     // start floor(256 r)/256 (host table): every earlier entry is
@@ -2732,6 +2743,8 @@ struct ipt_ctx {
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
+    int cdf_p2 = 0;
+    float cdf_p2s = 0.0f, cdf_end = 0.0f;
     int* d_cdf_lo = nullptr;  // cdf bucket starts (global light modes), null when a bucket is crowded
     bool any_round_light = false;
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
@@ -3233,6 +3246,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         // the extra LDS keeps, and gains 10 % on C5 (43.8 vs 40.2 Mpaths/s)
         kp.lnodes_lds = (ctx->lnodes_lds && ctx->n_light_nodes > 0 && ctx->n_light_nodes <= kLdsLightNodesMax) ? 1 : 0;
         kp.cdf_bsearch = ctx->cdf_bsearch;
+        kp.cdf_p2 = ctx->cdf_p2;
+        kp.cdf_p2s = ctx->cdf_p2s;
+        kp.cdf_end = ctx->cdf_end;
         kp.cdf_lo = ctx->d_cdf_lo;
         kp.lgrid = ctx->d_lgrid;
         kp.lax = reinterpret_cast<const float4*>(ctx->d_lax);
@@ -3638,6 +3654,24 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     lg.cells.clear();
     ctx->lgrid = lg;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
+    // nearly equal lights (e.g. 256 of one power: weights within rounding of
+    // 0.5/256 = 2^-9): with w = 2^-e and every light's |cdf[i] - (i+1) w| <= d
+    // < w/2 on a non-decreasing cdf, the first c with r < cdf[c] is ce - 1, ce
+    // or ce + 1 for ce = floor(r/w) = floor(r 2^e) (exact: r = m 2^-24): cdf[ce-2]
+    // <= (ce-1) w + d < ce w <= r and cdf[ce+1] >= (ce+2) w - d > r + w - d > r.
+    // Past the lights (ce >= nl) the scan's answer is ce's clamp to nl - 1, then
+    // cdf[nl]. The kernel reads cdf[ce-1] and cdf[ce] only.
+    ctx->cdf_p2 = 0;
+    for (int e = 1; IPT_CDF_POW2 && cdf_mono && nl > kLdsLights && !any_round && e <= 20 && !ctx->cdf_p2; ++e) {
+        const double w = std::ldexp(1.0, -e);
+        bool ok = (double)nl * w <= 1.0;
+        for (int i = 0; ok && i < nl; ++i) ok = std::fabs((double)cdf[i] - (double)(i + 1) * w) < 0.25 * w;
+        if (ok) {
+            ctx->cdf_p2 = 1;
+            ctx->cdf_p2s = std::ldexp(1.0f, e);
+            ctx->cdf_end = cdf[nl];
+        }
+    }
     ctx->any_round_light = any_round;
     // the axis-aligned single-light instances also take the range-free roots
     // and quotients: only where their ranges are proven (sphere-in-box scenes)

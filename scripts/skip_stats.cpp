@@ -36,6 +36,9 @@ static const Pol kPols[] = {
     {"no merge + pre-pop pre-skip, o<=6", 0xffffffffu, 6, 5, true, false},
     {"merge j<=1 + post-pop pre-skip (non-last), o<=6", 1, 6, 5, false, true},
     {"merge j<=1 + pre-pop and post-pop pre-skips, o<=6", 1, 6, 5, true, true},
+    {"12-word window: merge j<=1 + pre-pop pre-skip, o<=7 (j up to 6)", 1, 7, 6, true, false},
+    {"12-word window: merge j<=2 + pre-pop pre-skip, o<=7 (j up to 6)", 2, 7, 6, true, false},
+    {"12-word window: merge j<=1 + pre-pop pre-skip, o<=9 (j up to 8)", 1, 9, 8, true, false},
 };
 constexpr int kPol = sizeof(kPols) / sizeof(kPols[0]);
 

@@ -572,3 +572,35 @@ def test_c1_config_bit_exact(gpu_ctx, oracle):
         assert np.array_equal(_bits(img[k]), _bits(ref[k])), k
     assert np.array_equal(img["counters"], ref["counters"])
     assert abs(float(ref["pixels"].mean()) - 0.0654) < 0.002  # 0.06535 at 640^2
+
+
+def _jittered_powers(desc, rel, seed=3):
+    """desc with every light's power scaled by 1 + rel*u, u uniform in [-1, 1)."""
+    rng = np.random.default_rng(seed)
+    for L in desc["lights"]:
+        L["power"] = float(np.float32(L["power"]) * np.float32(1.0 + rel * (2.0 * rng.random() - 1.0)))
+    return desc
+
+
+@pytest.mark.parametrize("case", ["lattice_equal", "lattice_jitter", "random_jitter", "lattice_uneven"])
+def test_near_uniform_cdf_pick(gpu_ctx, oracle, case):
+    """The many-light pick from floor(r 2^e) and two cdf entries (IPT_CDF_POW2):
+    nearly equal powers (the 256-emitter lattice's own rounding, or powers
+    jittered by 1e-4 so that entries sit on both sides of (i+1) 2^-e), on the
+    lattice and on the light-BVH instance; and powers too uneven for it (the
+    bucket-table pick). Values and counters bit-exact against the oracle."""
+    desc = {"lattice_equal": lambda: scenes.make_scene_box_lights(16),
+            "lattice_jitter": lambda: _jittered_powers(scenes.make_scene_box_lights(16), 1e-4),
+            "random_jitter": lambda: _jittered_powers(
+                {**scenes.make_scene_random_lights(64), "lights": [
+                    {**L, "power": 0.5} for L in scenes.make_scene_random_lights(64)["lights"]]}, 1e-4),
+            "lattice_uneven": lambda: _jittered_powers(scenes.make_scene_box_lights(16), 0.5)}[case]()
+    W, H = 32, 24
+    gpu_ctx.upload_scene(desc)
+    gpu_ctx.reset_counters()
+    vals, _ = gpu_ctx.render_values(capi.make_params(W, H, 2, flags=capi.IPT_FLAG_COUNTERS))
+    g = gpu_ctx.counters()
+    ov, _, o = ob.render_values(desc, capi.make_params(W, H, 2), 0, with_counters=True)
+    assert np.array_equal(_bits(vals), _bits(ov))
+    for k in ("iterations", "light_samples", "skipped", "light_hits"):
+        assert g[k] == o[k], (case, k, g[k], o[k])
