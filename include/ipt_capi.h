@@ -116,7 +116,9 @@ typedef struct ipt_params {
     int32_t width, height;  /* GridRenderPlane size; render_sample hardcodes 640x640 */
     int32_t spp;            /* number of render_sample passes in this call */
     int32_t spp_offset;     /* absolute index of the first pass (RNG counter) */
-    int32_t n_rays;         /* branching factor of the root node (main.cpp:94), 0..255 */
+    int32_t n_rays;         /* branching factor of the root node (main.cpp:94), 0..65535
+                               (above 255: at most 8 suspended levels, i.e. depth_max <= 9
+                               once n_rays >= 512, and at most 65529 spheres) */
     int32_t depth_max;      /* main.cpp:95 */
     uint64_t seed;          /* Philox key */
     /* Destination-row sharding across devices: rows are cut into tiles of

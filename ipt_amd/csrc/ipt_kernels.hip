@@ -54,6 +54,7 @@ constexpr int kNumCounters = 15;
 
 struct KParams {
     int W, H, spp, spp_offset, n_rays, depth_max;
+    int meta_shift;  // a suspended level's meta word: ti | kind << meta_shift (8, or 16 for n_rays > 255)
     uint32_t key0, key1;
     int n_cand;              // candidate source rows
     const int* __restrict__ cand_rows;    // [n_cand] source row index
@@ -1430,9 +1431,10 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             const int meta = __float_as_int(s5);
             tpos = resume ? v3(s0, s1, s2) : tpos;
             tres = resume ? s3 + (s4 * 1.0f) * v : tres;  // res += multiplier*albedo*ray_power
-            ti = resume ? meta & 0xff : ti;
-            tkind = resume ? meta >> 8 : tkind;
-            need_frame = resume ? (meta >> 8) >= 5 && fdepth != stop : need_frame;
+            const int mkind = meta >> kp.meta_shift;
+            ti = resume ? meta & ((1 << kp.meta_shift) - 1) : ti;
+            tkind = resume ? mkind : tkind;
+            need_frame = resume ? mkind >= 5 && fdepth != stop : need_frame;
             tdepth = resume ? stop : tdepth;
             if (!resume) {
                 kp.values[unit] = v >= 0.0f ? v : 0.0f;  // main.cpp:214
@@ -1911,7 +1913,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     b[2 * kBlock] = tpos.z;
                     b[3 * kBlock] = tres;
                     b[4 * kBlock] = mult;
-                    b[5 * kBlock] = __int_as_float(ti | (tkind << 8));
+                    b[5 * kBlock] = __int_as_float(ti | (tkind << kp.meta_shift));
                 }
                 tpos = si_pos;
                 tkind = prim;
@@ -2978,6 +2980,7 @@ void candidate_rows(const ipt_params* p, std::vector<int>& rows, std::vector<int
     }
 }
 
+int needed_susp(const ipt_params* p);
 int validate(ipt_ctx* ctx, const ipt_params* p) {
     if (!ctx) return IPT_E_INVALID;
     if (!p) return fail(ctx, IPT_E_INVALID, "params is NULL");
@@ -2987,12 +2990,18 @@ int validate(ipt_ctx* ctx, const ipt_params* p) {
     if ((int64_t)p->width * p->height > (int64_t)1 << 31)
         return fail(ctx, IPT_E_INVALID, "frame larger than 2^31 pixels");
     if (p->spp < 0 || p->spp_offset < 0) return fail(ctx, IPT_E_INVALID, "negative spp");
-    // a suspended level stores its iteration count in the 8 low bits of its
-    // meta word (ti | kind << 8, ti <= n_rays), and n_rays < 256 bounds the
-    // pushed depth by 7 (a node at depth d has n_rays >> d children), so every
-    // depth_max fits the MAXSUSP = 8 instances
-    if (p->n_rays < 0 || p->n_rays > 255) return fail(ctx, IPT_E_UNSUPPORTED, "n_rays must be in [0,255]");
+    // a suspended level stores its iteration count in the low bits of its meta
+    // word (ti | kind << s, ti <= n_rays): s = 8 for n_rays < 256, else 16,
+    // which leaves 16 bits for the node kind (6 + sphere index)
+    if (p->n_rays < 0 || p->n_rays > 65535) return fail(ctx, IPT_E_UNSUPPORTED, "n_rays must be in [0,65535]");
+    if (p->n_rays > 255 && ctx->n_spheres > 65535 - 6)
+        return fail(ctx, IPT_E_UNSUPPORTED, "n_rays > 255 with more than 65529 spheres");
     if (p->depth_max < 0 || p->depth_max > 64) return fail(ctx, IPT_E_INVALID, "depth_max out of range");
+    // the deepest pushed node: n_rays < 256 bounds it by 7 (a node at depth d
+    // has n_rays >> d children) whatever depth_max; larger n_rays need
+    // depth_max <= 9 (the MAXSUSP = 8 instances)
+    if (needed_susp(p) > 8)
+        return fail(ctx, IPT_E_UNSUPPORTED, "n_rays > 255 with depth_max > 9: more than 8 suspended levels");
     if (p->n_shards > 1 && (p->shard_id < 0 || p->shard_id >= p->n_shards))
         return fail(ctx, IPT_E_INVALID, "shard_id out of range");
     return IPT_OK;
@@ -3130,8 +3139,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         rc = ensure_frame_table(ctx, st);
         if (rc) return rc;
     }
-    const int susp = needed_susp(p);
-    if (susp > 8) return fail(ctx, IPT_E_UNSUPPORTED, "recursion deeper than 8 suspended levels");
+    const int susp = needed_susp(p);  // <= 8 (validate)
     const bool count = (p->flags & IPT_FLAG_COUNTERS) != 0;
     for (int s0 = 0; s0 < p->spp; s0 += chunk) {
         const int ns = std::min(chunk, p->spp - s0);
@@ -3190,6 +3198,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.spp = ns;
         kp.spp_offset = p->spp_offset + s0;
         kp.n_rays = p->n_rays;
+        kp.meta_shift = p->n_rays > 255 ? 16 : 8;
         kp.depth_max = p->depth_max;
         kp.key0 = (uint32_t)p->seed;
         kp.key1 = (uint32_t)(p->seed >> 32);

@@ -107,11 +107,29 @@ def test_fractal_deep_bit_exact(gpu_ctx, oracle, n_rays, depth_max):
 
 
 def test_n_rays_limit(gpu_ctx):
-    """n_rays above the 8-bit iteration field is refused, not mis-rendered."""
+    """What the 16-bit iteration field and the 8-level instances cannot hold is
+    refused, not mis-rendered: n_rays above 65535, and trees deeper than 8
+    suspended levels (n_rays >= 512 with depth_max >= 11)."""
     gpu_ctx.upload_scene(scenes.make_scene_box())
-    with pytest.raises(capi.IptError) as e:
-        gpu_ctx.render_values(capi.make_params(4, 4, 1, n_rays=256, depth_max=2))
-    assert e.value.code == capi.IPT_E_UNSUPPORTED
+    for n, d in ((65536, 2), (1000, 11), (512, 11)):
+        with pytest.raises(capi.IptError) as e:
+            gpu_ctx.render_values(capi.make_params(4, 4, 1, n_rays=n, depth_max=d))
+        assert e.value.code == capi.IPT_E_UNSUPPORTED, (n, d)
+
+
+@pytest.mark.parametrize("scene,n,d", [("box", 256, 2), ("box", 300, 2), ("box", 1000, 2),
+                                       ("box", 511, 3), ("spheres300", 260, 2)])
+def test_wide_n_rays_bit_exact(gpu_ctx, oracle, scene, n, d):
+    """n_rays above 255 (the reference takes any int from argv, main.cpp:239-243):
+    the suspended level's iteration count in 16 bits, the node kind (6 + sphere
+    index on the sphere-list scene) above it; power-of-two and other n."""
+    desc = scenes.make_scene_box() if scene == "box" else scenes.make_scene_spheres(300)
+    gpu_ctx.upload_scene(desc)
+    p = capi.make_params(4, 3, 1, n_rays=n, depth_max=d)
+    vals, codes = gpu_ctx.render_values(p)
+    ov, oc = ob.render_values(desc, p)
+    assert np.array_equal(vals.view(np.uint32), ov.view(np.uint32))
+    assert np.array_equal(codes, oc)
 
 
 def _duplicated_lattice(k, r, dup_stride):
