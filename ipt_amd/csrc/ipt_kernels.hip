@@ -2353,10 +2353,31 @@ __global__ __launch_bounds__(256) void accumulate_kernel(AParams ap) {
         int r0 = H - 2 - yi;
         const int c0 = r0 >= 0 ? ap.cand_of_row[r0] : -1;
         const int c1 = (yi == 0 && H >= 1) ? ap.cand_of_row[H - 1] : -1;
-        for (int sp = 0; sp < ap.spp; ++sp) {
+        // the samples' loads issued 8 passes at a time, then the 8 running-mean
+        // updates in the same order: one load latency per 8 passes instead of
+        // one per pass (the updates are a serial chain per pixel)
+        const bool t0 = c0 >= 0, t1 = c1 >= 0 && c1 != c0;
+        const float* v0p = ap.values + (size_t)(t0 ? c0 : 0) * ap.W + xi;
+        const float* v1p = ap.values + (size_t)(t1 ? c1 : 0) * ap.W + xi;
+        int sp = 0;
+        for (; sp + 8 <= ap.spp; sp += 8) {
+            float a0[8], a1[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const size_t base = (size_t)(sp + q) * pass_stride;
+                a0[q] = t0 ? v0p[base] : 0.0f;
+                a1[q] = t1 ? v1p[base] : 0.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (t0) add_ray(a0[q], p, c, s, m);
+                if (t1) add_ray(a1[q], p, c, s, m);
+            }
+        }
+        for (; sp < ap.spp; ++sp) {
             const size_t base = (size_t)sp * pass_stride;
-            if (c0 >= 0) add_ray(ap.values[base + (size_t)c0 * ap.W + xi], p, c, s, m);
-            if (c1 >= 0 && c1 != c0) add_ray(ap.values[base + (size_t)c1 * ap.W + xi], p, c, s, m);
+            if (t0) add_ray(v0p[base], p, c, s, m);
+            if (t1) add_ray(v1p[base], p, c, s, m);
         }
     } else {
         int rows[4];
