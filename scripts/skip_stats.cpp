@@ -1,9 +1,11 @@
 // Analysis tool (not product code): replays C2 paths through the oracle and
 // classifies the iterations whose light pick is a certain skip (the node lies
 // behind the light's plane), to price skip-merging policies of the path
-// kernel's step loop before writing them. Build and run:
-//   g++ -O2 -std=c++17 -fopenmp -Iinclude -Iipt_amd/host scripts/skip_stats.cpp \
-//       ipt_amd/host/sample_scenes.cpp ipt_amd/host/ipt_host.cpp -o /tmp/skip_stats && /tmp/skip_stats 256 8
+// kernel's step loop before writing them (it links the C-ABI library only for
+// the host layer's scene builder; no GPU is used). Build and run:
+//   g++ -O2 -std=c++17 -Iinclude -Iipt_amd/host scripts/skip_stats.cpp ipt_amd/host/ipt_host.cpp \
+//       -o /tmp/skip_stats -lpthread -L ipt_amd/lib -lipt_hip -Wl,-rpath,$PWD/ipt_amd/lib
+//   /tmp/skip_stats 128 4      # 128x128 pixels, 4 passes of sample_scenes[0]
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
