@@ -116,8 +116,9 @@ IPT_HD Frame make_frame_sc_fast(vec3 to, float s, float c, bool& ok) {
     const float r20 = s * ay, r21 = -(s * ax), r22 = c;
     // q >= 2^-80 and r >= 1e-6: the exact path's axis is not replaced; q
     // finite: `to` is finite (a NaN/inf component reaches q)
+    // (|r20| = |r02| and |r21| = |r12|: negations of the same products)
     const float mn = fminf(fminf(fminf(fabs_(r00), fabs_(r01)), fminf(fabs_(r02), fabs_(r10))),
-                           fminf(fminf(fabs_(r11), fabs_(r12)), fminf(fabs_(r21), fabs_(r22))));
+                           fminf(fminf(fabs_(r11), fabs_(r12)), fabs_(r22)));
     ok = (mn > 0.0f) & (q >= 0x1p-80f) & (q < inf_()) & !lt_1em6(r);
     mat3 M;
     M.c[0] = v3(r00, r01, r02);
