@@ -102,6 +102,10 @@ struct KParams {
     // skip-ahead (prologue): every light sample's point lies on the plane z =
     // sa_pz and the light normal is (+-0, +-0, sa_nz): light picks at nodes
     // with sa_nz * (sa_pz - z) >= 0 are certain skips (sa_on, host-checked)
+    // u01(w) < c  <=>  w < (ceil(c 2^24) << 8) (clamped to [0, 2^32]) for the
+    // draw word w: the single light's cdf[0], cdf[1] (pk_u0, pk_u1) and sa_cl
+    // (sa_u) as word thresholds (host: word_threshold)
+    unsigned long long pk_u0, pk_u1, sa_u;
     int sa_on;
     float sa_pz, sa_nz;
     // a pick r < sa_cl is a light pick (one light: cdf[0]; a lattice with a
@@ -1555,7 +1559,13 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             // took the next pick's skip may end 9 words past blk, so after the
             // one shift j <= 5 (words j .. j+2 are still in the window)
             const uint32_t j = kPreSkip ? k - 4u * blk : k & 3u;
-            const float r = u01(kPreSkip && j >= 4u ? (j & 1u ? w.b1 : w.b0) : sel4(j & 3u, w.a0, w.a1, w.a2, w.a3));
+            const uint32_t rw = kPreSkip && j >= 4u ? (j & 1u ? w.b1 : w.b0) : sel4(j & 3u, w.a0, w.a1, w.a2, w.a3);
+            const float r = u01(rw);
+            // the single light's pick on the raw word: r < cdf[c] as w < pk_u (host-exact)
+            auto pick_w = [&](uint32_t wd) {
+                return (unsigned long long)wd < kp.pk_u0 ? 0 : ((unsigned long long)wd < kp.pk_u1 ? 1 : 2);
+            };
+            constexpr bool kPickInt = IPT_PICK_INT && one_light(LMODE);
             // UnionDdf::sample's component: the first c with r < cdf[c] (ddf.cpp:142-153)
             auto pick_of = [&](float r) {
                 int c = 0;
@@ -1602,7 +1612,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 }
                 return c;
             };
-            int c = pick_of(r);
+            int c = kPickInt ? pick_w(rw) : pick_of(r);
             uint32_t jj = j;  // the window offset of the iteration's pick (skip-ahead: j + 3)
             if constexpr (kSkipAhead) {
                 // A light pick at a node on the lights' back side is a certain
@@ -1635,7 +1645,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     if (COUNT) { ++c_iter; ++c_lsamp; ++c_skip; }
                     k += 3;
                     jj = j + 3u;
-                    c = pick_of(u01(j == 0u ? w.a3 : w.b0));  // word j + 3
+                    c = kPickInt ? pick_w(j == 0u ? w.a3 : w.b0) : pick_of(u01(j == 0u ? w.a3 : w.b0));  // word j + 3
                 }
             }
             pick = c;
@@ -2262,7 +2272,8 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             // same order, same counts.
             // (as selects: no exec-mask branch)
             const bool back = (tpos.z - kp.sa_pz) * kp.sa_nz < 0.0f;
-            const bool take = iter_lane && pre_ok && back && ti < (kp.n_rays >> tdepth) && u01(pre_w) < kp.sa_cl;
+            const bool lpick = IPT_PICK_INT ? (unsigned long long)pre_w < kp.sa_u : u01(pre_w) < kp.sa_cl;
+            const bool take = iter_lane && pre_ok && back && ti < (kp.n_rays >> tdepth) && lpick;
             ti += take ? 1 : 0;
             k += take ? 3u : 0u;
             if (COUNT) {
@@ -2772,6 +2783,7 @@ struct ipt_ctx {
     bool any_round_light = false;
     int light_axis = 0;  // axis_aligned_light() of a single AreaLight (kLightsOneA10/A01)
     LightGrid lgrid;     // lgrid.pattern != 0: coplanar light lattice (kLightsGridA10/A01)
+    unsigned long long pk_u0 = 0, pk_u1 = 0, sa_u = 0;  // word thresholds (KParams)
     int sa_on = 0;       // the lights' sample points share the plane z = sa_pz, normal (0, 0, sa_nz) (skip-ahead)
     float sa_pz = 0.0f, sa_nz = 0.0f, sa_cl = 0.0f;
     int* d_lgrid = nullptr;
@@ -2999,6 +3011,17 @@ void candidate_rows(const ipt_params* p, std::vector<int>& rows, std::vector<int
             rows.push_back(iy);
         }
     }
+}
+
+// The draw word w's u01(w) = (w >> 8) 2^-24 is below c exactly when w >> 8 <
+// T = ceil(c 2^24) (both sides exact: an integer against c scaled by a power
+// of two), i.e. when w < T << 8: T = 0 for c <= 0 or NaN (never), 2^24 for
+// c >= 1 (always, as a 64-bit bound).
+unsigned long long word_threshold(float c) {
+    const double x = (double)c * 16777216.0;
+    if (!(x > 0.0)) return 0ull;
+    if (x >= 16777216.0) return 1ull << 32;
+    return (unsigned long long)std::ceil(x) << 8;
 }
 
 int needed_susp(const ipt_params* p);
@@ -3289,6 +3312,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.lg_icw = ctx->lgrid.icw;
         kp.lg_ich = ctx->lgrid.ich;
         kp.lg_e = ctx->lgrid.e;
+        kp.pk_u0 = ctx->pk_u0;
+        kp.pk_u1 = ctx->pk_u1;
+        kp.sa_u = ctx->sa_u;
         kp.sa_on = ctx->sa_on;
         kp.sa_pz = ctx->sa_pz;
         kp.sa_nz = ctx->sa_nz;
@@ -3684,6 +3710,8 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     lg.cells.clear();
     ctx->lgrid = lg;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
+    ctx->pk_u0 = word_threshold(cdf[0]);
+    ctx->pk_u1 = word_threshold(nl >= 1 ? cdf[1] : 0.0f);
     // nearly equal lights (e.g. 256 of one power: weights within rounding of
     // 0.5/256 = 2^-9): with w = 2^-e and every light's |cdf[i] - (i+1) w| <= d
     // < w/2 on a non-decreasing cdf, the first c with r < cdf[c] is ce - 1, ce
@@ -3730,6 +3758,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
             // c < nl, i.e. iff r < cdf[nl - 1] on a non-decreasing cdf
             ctx->sa_cl = (nl == 1 || cdf_mono) ? cdf[nl - 1] : 0.0f;
         }
+        ctx->sa_u = word_threshold(ctx->sa_on ? ctx->sa_cl : 0.0f);
     }
     ctx->d_bvh_nodes = n_bvh_nodes.release();
     ctx->d_bvh_prims = n_bvh_prims.release();
