@@ -1503,7 +1503,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 if (ran && gcos) {
                     tr = kp.cos_a[gi_a];
                     float sp, cp;
-                    sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
+                    sincosf_small_(two_pi_times_u24(gi_b), &sp, &cp);
                     cs_c = cp;
                     cs_s = sp;
                 }
@@ -1538,7 +1538,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     cs_s = cb.y;
                 } else {
                     float sp, cp;
-                    sincosf_small_(two_pi_times(u01(gi_b << 8)), &sp, &cp);
+                    sincosf_small_(two_pi_times_u24(gi_b), &sp, &cp);
                     cs_c = cp;
                     cs_s = sp;
                 }

@@ -498,6 +498,10 @@ IPT_HD float div_pi_to_f32(float z) { return (float)((double)z * u2d(0x3fd45f306
 
 // CosineDdf::sample phi (ddf.cpp:228): (float)(2*M_PI*(double)u2)
 IPT_HD float two_pi_times(float u) { return (float)(u2d(0x401921fb54442d18ull) * (double)u); }
+// two_pi_times(u01(g << 8)) for a 24-bit g: u = g 2^-24 exactly, so the double
+// product 2pi * u is RN(2pi * g * 2^-24) = RN((2pi 2^-24) * g) -- the same
+// real product, the constant scaled by a power of two -- from g directly
+IPT_HD float two_pi_times_u24(uint32_t g) { return (float)(u2d(0x3e9921fb54442d18ull) * (double)g); }
 
 // ------------------------------------------------------------ RNG (Philox)
 // Philox4x32-10 (Salmon et al., SC'11; Random123 constants).

@@ -103,3 +103,18 @@ def test_frame_angle_and_range_free_root(libm):
         sweep(libm, F[fn], 0, 0x3f800001)
         sweep(libm, F[fn], 0x80000000, 0xbf800001)
     sweep(libm, F["sqrt_inrange"], 0, 0x7f800000)
+
+
+def test_two_pi_times_from_24_bit_draw():
+    """two_pi_times_u24(g) (ipt_math.h) == two_pi_times(u01(g << 8)) for every
+    24-bit g: (float)(2pi * (g 2^-24)) in double equals (float)((2pi 2^-24) *
+    g), the same real product with the constant scaled by a power of two."""
+    import struct
+    two_pi = struct.unpack("<d", struct.pack("<Q", 0x401921FB54442D18))[0]
+    scaled = struct.unpack("<d", struct.pack("<Q", 0x3E9921FB54442D18))[0]
+    assert scaled == two_pi * 2.0 ** -24
+    g = np.arange(1 << 24, dtype=np.uint64)
+    u = g.astype(np.float32) * np.float32(2.0 ** -24)
+    a = (two_pi * u.astype(np.float64)).astype(np.float32)
+    b = (scaled * g.astype(np.float64)).astype(np.float32)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
