@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define IPT_ABI_VERSION 4
+#define IPT_ABI_VERSION 5
 
 enum {
     IPT_OK = 0,
@@ -197,8 +197,19 @@ void ipt_destroy(ipt_ctx* ctx);
    half-uploaded one; upload again to recover. */
 int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* scene);
 
-/* Host buffers: copies the image in, renders p->spp passes, copies it out. */
+/* Host buffers (the caller's GridRenderPlane state): renders p->spp passes
+   into them. Device-resident: the context keeps the rows this call
+   accumulates -- every row, or with p->n_shards > 1 the shard's owned tiles
+   (ipt_shard_plan) -- on its device across calls, uploads only the owned rows
+   whose host bytes changed since it last returned them (none in a
+   progressive loop that leaves the plane alone between calls) and downloads
+   only the owned rows: 16 B per owned pixel per call with sums and per-pixel
+   max, 8 B without. Rows it does not own are neither read nor written, so the
+   contexts of a multi-device render can share one host plane (one thread per
+   context). Results are identical to copying the whole image each way. */
 int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* host_img);
+/* Bytes the last ipt_render moved host -> device and device -> host. */
+int ipt_transfer_bytes(ipt_ctx* ctx, uint64_t* host_to_device, uint64_t* device_to_host);
 
 /* Device buffers (hipMalloc'd or torch CUDA tensors). The GridRenderPlane
    replays run on `hip_stream` (NULL = the context's own stream) after the work
@@ -315,7 +326,13 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
          1.0f / x sequence (three corrections)
       19 / 20 (ipt_math_selfcheck only) the range-free division against
          IEEE a/b over the division pairs of 10 / pairs whose divisors have
-         all-ones-like significands */
+         all-ones-like significands
+      21 (ipt_math_selfcheck only) the range-free division against IEEE a/b
+         over every pair of significands (a, b in [1, 2)): pattern indices
+         up to 2^46, i = (a's significand << 23) | b's; first_bad reports
+         the a significand (i >> 23)
+      22 (ipt_math_selfcheck only) the range-free reciprocal's exact scaling:
+         rcp(b) == sign(b) 2^-e rcp(m) for |b| = m 2^e in [2^-40, 2^41) */
 int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 /* Philox4x32-10 blocks exactly as the kernels generate the per-path stream
    that replaces randf() (include/randf.h:6-11; draw k of path (pass s, pixel
@@ -325,7 +342,7 @@ int ipt_math_host(int fn, const float* in, float* out, int64_t n);
 int ipt_philox(ipt_ctx* ctx, uint32_t key0, uint32_t key1, const uint32_t* ctr, uint32_t* out, int64_t n);
 int ipt_math_device(ipt_ctx* ctx, int fn, const float* in, float* out, int64_t n);
 /* Device self-check of the fast math paths: for every float bit pattern b in
- * [lo_bits, hi_bits) (hi_bits <= 2^32) compares function fn as the kernels
+ * [lo_bits, hi_bits) (hi_bits <= 2^32; 2^46 for fn 21) compares function fn as the kernels
  * compute it with its exact restatement, on the device. Returns the number of
  * differing results (NaN == NaN) and the lowest differing pattern (0xffffffff
  * if none). Used to prove a fast path exhaustively (all 2^32 inputs). */

@@ -8,6 +8,7 @@
 #include <GridRenderPlane.h>
 #include <sample_scenes.h>
 
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
@@ -17,6 +18,7 @@
 void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
                         int depth_max, uint64_t seed);
 int render_gpu_uploads();
+uint64_t render_gpu_last_transfer();
 void render_gpu_release();
 void render_samples_multi_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
                               int depth_max, uint64_t seed, const std::vector<int>& devices, int tile_rows);
@@ -63,6 +65,7 @@ int main(int argc, char** argv) {
         return 3;
     }
     const int uploads = render_gpu_uploads();
+    const unsigned long long transfer = render_gpu_last_transfer();
     render_gpu_release();
     std::vector<unsigned> cnt(plane.pixel_counters.begin(), plane.pixel_counters.end());
     const std::string pre = argv[6];
@@ -72,6 +75,6 @@ int main(int argc, char** argv) {
     f = std::fopen((pre + ".u32").c_str(), "wb");
     std::fwrite(cnt.data(), 4, cnt.size(), f);
     std::fclose(f);
-    std::printf("max_value %.9g uploads %d\n", plane.max_value, uploads);
+    std::printf("max_value %.9g uploads %d last_call_transfer_bytes %llu\n", plane.max_value, uploads, transfer);
     return 0;
 }

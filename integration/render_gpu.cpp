@@ -153,12 +153,16 @@ public:
     GpuRenderer(const GpuRenderer&) = delete;
     GpuRenderer& operator=(const GpuRenderer&) = delete;
 
-    // spp passes of render_sample into `plane`, continuing its running means
-    // (GridRenderPlane::addRay semantics, bit-exact against the CPU restatement);
-    // with n_shards > 1 only the destination rows of tile shard `shard_id`
-    // (16-row tiles dealt round-robin, ipt_shard_plan) are rendered and written
-    void render(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays, int depth_max,
-                uint64_t seed, int n_shards = 1, int shard_id = 0, int tile_rows = 16) {
+    // spp passes of render_sample into the C-ABI image `img` (the plane's
+    // pixels, 32-bit counters, per-pixel running max), continuing its running
+    // means (GridRenderPlane::addRay semantics, bit-exact against the CPU
+    // restatement); with n_shards > 1 only the destination rows of tile shard
+    // `shard_id` (tile_rows-row tiles dealt round-robin, ipt_shard_plan) are
+    // rendered, read and written. The context keeps its rows on its device
+    // between calls (ipt_render), so a call moves only those rows.
+    void render_image(const Scene& scene, ipt_image& img, int width, int height, int spp, int spp_offset,
+                      int n_rays, int depth_max, uint64_t seed, int n_shards = 1, int shard_id = 0,
+                      int tile_rows = 16) {
         Flat f;
         flatten(scene, f);
         if (!has_scene_ || !(f == last_)) {
@@ -171,8 +175,8 @@ public:
             ++uploads_;
         }
         ipt_params p{};
-        p.width = (int)plane.width;
-        p.height = (int)plane.height;
+        p.width = width;
+        p.height = height;
         p.spp = spp;
         p.spp_offset = spp_offset;
         p.n_rays = n_rays;
@@ -183,13 +187,12 @@ public:
             p.n_shards = n_shards;
             p.shard_id = shard_id;
         }
-        // GridRenderPlane counts in size_t; the library in uint32 (< 2^32 passes)
-        std::vector<uint32_t> cnt(plane.pixel_counters.begin(), plane.pixel_counters.end());
-        std::vector<float> pmax(plane.pixels.size(), 0.0f);
-        ipt_image img{plane.pixels.data(), cnt.data(), nullptr, pmax.data()};
         if (ipt_render(ctx_, &p, &img) != IPT_OK) throw std::runtime_error(ipt_last_error(ctx_));
-        std::copy(cnt.begin(), cnt.end(), plane.pixel_counters.begin());
-        for (float m : pmax) plane.max_value = std::max(plane.max_value, m);
+    }
+    uint64_t transferred() const {  // host <-> device bytes of the last call
+        uint64_t a = 0, b = 0;
+        if (ipt_transfer_bytes(ctx_, &a, &b) != IPT_OK) throw std::runtime_error(ipt_last_error(ctx_));
+        return a + b;
     }
     int uploads() const { return uploads_; }
 
@@ -200,15 +203,46 @@ private:
     int uploads_ = 0;
 };
 
-// The free-function form of INTEGRATION.md §1 on a process-wide renderer,
-// released by render_gpu_release() (call it before exit: the HIP runtime may
-// be torn down before static destructors run).
-static std::unique_ptr<GpuRenderer> g_renderer;
+// GridRenderPlane (size_t counters, GridRenderPlane.h) <-> the C-ABI image:
+// 32-bit counters and a zeroed per-pixel running max for this call
+struct PlaneIo {
+    std::vector<uint32_t> cnt;
+    std::vector<float> pmax;
+    explicit PlaneIo(const GridRenderPlane& plane)
+        : cnt(plane.pixel_counters.begin(), plane.pixel_counters.end()), pmax(plane.pixels.size(), 0.0f) {}
+    ipt_image image(GridRenderPlane& plane) { return ipt_image{plane.pixels.data(), cnt.data(), nullptr, pmax.data()}; }
+    void finish(GridRenderPlane& plane) const {
+        std::copy(cnt.begin(), cnt.end(), plane.pixel_counters.begin());
+        for (float m : pmax) plane.max_value = std::max(plane.max_value, m);
+    }
+};
+
+// The free-function form of INTEGRATION.md §1 on process-wide renderers, one
+// per device, released by render_gpu_release() (call it before exit: the HIP
+// runtime may be torn down before static destructors run).
+static std::vector<std::pair<int, std::unique_ptr<GpuRenderer>>> g_single;
+static uint64_t g_last_transfer = 0;
+
+static GpuRenderer& single_renderer(int device) {
+    for (auto& e : g_single)
+        if (e.first == device) return *e.second;
+    g_single.emplace_back(device, std::make_unique<GpuRenderer>(device));
+    return *g_single.back().second;
+}
+
+static void render_on(int device, const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
+                      int depth_max, uint64_t seed) {
+    GpuRenderer& r = single_renderer(device);
+    PlaneIo io(plane);
+    ipt_image img = io.image(plane);
+    r.render_image(scene, img, (int)plane.width, (int)plane.height, spp, spp_offset, n_rays, depth_max, seed);
+    io.finish(plane);
+    g_last_transfer = r.transferred();
+}
 
 void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int spp_offset, int n_rays,
                         int depth_max, uint64_t seed) {
-    if (!g_renderer) g_renderer = std::make_unique<GpuRenderer>(0);
-    g_renderer->render(scene, plane, spp, spp_offset, n_rays, depth_max, seed);
+    render_on(0, scene, plane, spp, spp_offset, n_rays, depth_max, seed);
 }
 
 
@@ -216,9 +250,9 @@ void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, int spp, int
 // plane, src/main.cpp:256-285): one context per entry of `devices` (a device
 // may repeat), destination rows cut into `tile_rows`-row tiles dealt
 // round-robin to the contexts (ipt_params.n_shards / shard_id), each context
-// driven by its own host thread on a private copy of the plane, and the
-// owned rows of every shard copied back into the caller's plane at the end of
-// the call (every pixel has exactly one owner, so no arithmetic merges them).
+// driven by its own host thread straight into the caller's plane: ipt_render
+// reads and writes only the context's own rows, which its device keeps
+// between calls, so every pixel has exactly one owner and nothing is merged.
 // Each shard traces only the samples that can land in its rows, with the same
 // (seed, pass, pixel) streams, so the plane is bit-identical to the
 // one-device render.
@@ -229,8 +263,8 @@ void render_samples_multi_gpu(const Scene& scene, GridRenderPlane& plane, int sp
                               int depth_max, uint64_t seed, const std::vector<int>& devices, int tile_rows) {
     const int n = (int)devices.size();
     if (n == 0) throw std::runtime_error("render_samples_multi_gpu: no devices");
-    if (n == 1) {
-        render_samples_gpu(scene, plane, spp, spp_offset, n_rays, depth_max, seed);
+    if (n == 1) {  // the listed device, not device 0
+        render_on(devices[0], scene, plane, spp, spp_offset, n_rays, depth_max, seed);
         return;
     }
     if (g_multi_devices != devices) {
@@ -238,14 +272,16 @@ void render_samples_multi_gpu(const Scene& scene, GridRenderPlane& plane, int sp
         for (int d : devices) g_multi.push_back(std::make_unique<GpuRenderer>(d));
         g_multi_devices = devices;
     }
-    const size_t W = plane.width, H = plane.height;
-    std::vector<GridRenderPlane> part(n, plane);
+    PlaneIo io(plane);
+    const ipt_image img = io.image(plane);
     std::vector<std::string> err(n);
     std::vector<std::thread> th;
     for (int k = 0; k < n; ++k)
         th.emplace_back([&, k] {
             try {
-                g_multi[k]->render(scene, part[k], spp, spp_offset, n_rays, depth_max, seed, n, k, tile_rows);
+                ipt_image im = img;
+                g_multi[k]->render_image(scene, im, (int)plane.width, (int)plane.height, spp, spp_offset, n_rays,
+                                         depth_max, seed, n, k, tile_rows);
             } catch (const std::exception& e) {
                 err[k] = e.what();
             }
@@ -253,37 +289,25 @@ void render_samples_multi_gpu(const Scene& scene, GridRenderPlane& plane, int sp
     for (auto& t : th) t.join();
     for (int k = 0; k < n; ++k)
         if (!err[k].empty()) throw std::runtime_error(err[k]);
-    ipt_params q{};
-    q.width = (int)W;
-    q.height = (int)H;
-    q.tile_rows = tile_rows;
-    q.n_shards = n;
-    std::vector<uint8_t> owned(H);
-    std::vector<int32_t> cand(H);
-    int32_t n_cand = 0;
-    for (int k = 0; k < n; ++k) {
-        q.shard_id = k;
-        if (ipt_shard_plan(&q, owned.data(), cand.data(), &n_cand) != IPT_OK)
-            throw std::runtime_error(ipt_last_error(nullptr));
-        for (size_t y = 0; y < H; ++y)
-            if (owned[y]) {
-                std::copy_n(part[k].pixels.begin() + y * W, W, plane.pixels.begin() + y * W);
-                std::copy_n(part[k].pixel_counters.begin() + y * W, W, plane.pixel_counters.begin() + y * W);
-            }
-        plane.max_value = std::max(plane.max_value, part[k].max_value);
-    }
+    io.finish(plane);
+    g_last_transfer = 0;
+    for (const auto& r : g_multi) g_last_transfer += r->transferred();
 }
+
+// host <-> device bytes of the last render call (all its contexts)
+uint64_t render_gpu_last_transfer() { return g_last_transfer; }
 
 // scene uploads of the most-uploaded context (1 when an unchanged scene is
 // rendered progressively)
 int render_gpu_uploads() {
-    int u = g_renderer ? g_renderer->uploads() : 0;
+    int u = 0;
+    for (const auto& e : g_single) u = std::max(u, e.second->uploads());
     for (const auto& r : g_multi) u = std::max(u, r->uploads());
     return u;
 }
 
 void render_gpu_release() {
-    g_renderer.reset();
+    g_single.clear();
     g_multi.clear();
     g_multi_devices.clear();
 }

@@ -69,8 +69,8 @@ class Image(C.Structure):
                 ("pixel_max", C.c_void_p)]
 
 
-ABI_VERSION = 4  # include/ipt_capi.h IPT_ABI_VERSION
-ABI_LAYOUT_COMPATIBLE = (3, 4)  # versions with this binding's struct layouts (IPT_ABI_COMPAT only)
+ABI_VERSION = 5  # include/ipt_capi.h IPT_ABI_VERSION
+ABI_LAYOUT_COMPATIBLE = (3, 4, 5)  # versions with this binding's struct layouts (IPT_ABI_COMPAT only)
 
 COUNTER_NAMES = ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
                  "iterations", "light_samples", "skipped", "sphere_frames", "light_traces",
@@ -90,7 +90,7 @@ EXPORTED_SYMBOLS = (
     "ipt_get_counters",
     "ipt_reset_counters", "ipt_last_kernel_ms", "ipt_math_host", "ipt_math_device",
     "ipt_shard_plan", "ipt_get_profile", "ipt_math_selfcheck", "ipt_smooth", "ipt_glare", "ipt_ddf_sample", "ipt_ddf_value",
-    "ipt_philox",
+    "ipt_philox", "ipt_transfer_bytes",
 )
 
 # path-kernel phases of the IPT_PROF profile (ipt_kernels.hip IPT_PHASE ids)
@@ -140,6 +140,8 @@ def load(path: str | os.PathLike | None = None):
     if hasattr(lib, "ipt_render_device_async"):
         lib.ipt_render_device_async.argtypes = [C.c_void_p, C.POINTER(Params), C.POINTER(Image), C.c_void_p]
         lib.ipt_render_wait.argtypes = [C.c_void_p]
+    if hasattr(lib, "ipt_transfer_bytes"):
+        lib.ipt_transfer_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     lib.ipt_render_values.argtypes = [C.c_void_p, C.POINTER(Params), C.c_void_p, C.c_void_p]
     lib.ipt_get_counters.argtypes = [C.c_void_p, C.POINTER(Counters)]
     lib.ipt_reset_counters.argtypes = [C.c_void_p]
@@ -250,6 +252,12 @@ class Context:
         im.sums = img["sums"].ctypes.data if img.get("sums") is not None else None
         im.pixel_max = img["pixel_max"].ctypes.data if img.get("pixel_max") is not None else None
         _check(self.lib, self.h, self.lib.ipt_render(self.h, C.byref(p), C.byref(im)))
+
+    def transfer_bytes(self) -> tuple[int, int]:
+        """(host -> device, device -> host) bytes of the last render() call."""
+        h2d, d2h = C.c_uint64(), C.c_uint64()
+        _check(self.lib, self.h, self.lib.ipt_transfer_bytes(self.h, C.byref(h2d), C.byref(d2h)))
+        return int(h2d.value), int(d2h.value)
 
     def render_device(self, p: Params, pixels_ptr, counters_ptr, sums_ptr=None, max_ptr=None,
                       stream=None):
@@ -375,6 +383,9 @@ SELFCHECK_FRAME_FAST = 16  # ipt_math_selfcheck only: fast vs exact sphere-in-bo
 # ipt_math_selfcheck only: reciprocal with 1 / 2 Newton corrections vs the round-4 three-correction
 # sequence; the range-free division vs IEEE over the division pairs / near-all-ones divisors
 SELFCHECK_RCP1, SELFCHECK_RCP2, SELFCHECK_DIV_PAIRS, SELFCHECK_DIV_ONES = 17, 18, 19, 20
+# ipt_math_selfcheck only: the range-free division over every pair of significands (pattern
+# indices up to 2^46) and the reciprocal's exact scaling over the range (all 2^32 floats)
+SELFCHECK_DIV_ALL_SIGNIFICANDS, SELFCHECK_RCP_SCALING = 21, 22
 
 
 def shard_plan(p: Params):

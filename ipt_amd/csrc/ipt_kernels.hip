@@ -1435,7 +1435,9 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             const int meta = __float_as_int(s5);
             tpos = resume ? v3(s0, s1, s2) : tpos;
             tres = resume ? s3 + (s4 * 1.0f) * v : tres;  // res += multiplier*albedo*ray_power
-            const int mkind = meta >> kp.meta_shift;
+            // (unsigned: with n_rays > 255 a kind of 6 + sphere index >= 32768
+            // sets bit 31 of the word, which must not sign-extend)
+            const int mkind = (int)((uint32_t)meta >> kp.meta_shift);
             ti = resume ? meta & ((1 << kp.meta_shift) - 1) : ti;
             tkind = resume ? mkind : tkind;
             need_frame = resume ? mkind >= 5 && fdepth != stop : need_frame;
@@ -1706,6 +1708,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     to = pto;
                     fs = pfs;
                     fc = pfc;
+                    if constexpr (!IPT_FRAME_FB_PF) {
                     if (__builtin_expect(__any(!pfok), 0))
                         if (!pfok) {
                             to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
@@ -1713,6 +1716,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                             keep_alive(fs);  // its wait stays in this rare branch
                             keep_alive(fc);
                         }
+                    }
                     pfok = false;
                 } else {
                     to = kFrameInrange ? normalize_inrange_(nrm) : normalize(nrm);
@@ -1923,7 +1927,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     b[2 * kBlock] = tpos.z;
                     b[3 * kBlock] = tres;
                     b[4 * kBlock] = mult;
-                    b[5 * kBlock] = __int_as_float(ti | (tkind << kp.meta_shift));
+                    b[5 * kBlock] = __uint_as_float((uint32_t)ti | ((uint32_t)tkind << kp.meta_shift));
                 }
                 tpos = si_pos;
                 tkind = prim;
@@ -2101,11 +2105,14 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             if (COUNT) c_ltr += (uint32_t)nl * ((is_iter ? 1u : 0u) + ((rdepth < kp.depth_max) ? 1u : 0u));
             if constexpr (grid_lights(LMODE)) {
                 // the ray's point on the lights' plane and its cell(s): every
-                // light whose exact test can pass lies in a cell within 2^-8
-                // cells of that point (light_grid_build's lattice tolerance and
-                // the rounding of u, v are far below it), so the lights of those
-                // <= 4 cells, in index order, are the scan's hits (a light that
-                // is not hit adds +0 to lmix and is never nearest)
+                // light whose exact test can pass lies in a cell within
+                // kp.lg_e cells of that point (LightGrid::e, derived per
+                // lattice by light_grid_build in ipt_path.h from the lattice's
+                // tolerance and the rounding of u, v; as small as 2^-14 -- it
+                // holds because the light tests below take the same plane
+                // point q as this lookup), so the lights of those <= 4 cells,
+                // in index order, are the scan's hits (a light that is not hit
+                // adds +0 to lmix and is never nearest)
                 constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
                 // (the lattice's ranges are proven like the single light's,
                 // light_ranges_box: the range-free quotient of light_trace_ax,
@@ -2298,6 +2305,15 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                         pfs = e.x;
                         pfc = e.y;
                         pto = to;
+                    }
+                    if constexpr (IPT_FRAME_FB_PF) {
+                        // the out-of-table angle computed here as well, so that
+                        // the frame phase reads `to`, sin a, cos a unconditionally
+                        if (__builtin_expect(__any(!pfok), 0))
+                            if (!pfok) {
+                                frame_angle_sc(to, &pfs, &pfc);
+                                pto = to;
+                            }
                     }
                 }
             }
@@ -2679,6 +2695,46 @@ __device__ bool frame_fast_mismatch(uint32_t b) {
     return diff;
 }
 
+// fn 21: the range-free division over EVERY pair of significands, a and b in
+// [1, 2) (index i: a = 1 + (i >> 23) 2^-23, b = 1 + (i & (2^23 - 1)) 2^-23,
+// 2^46 pairs), against IEEE a/b. With fn 22 (the reciprocal scales exactly)
+// this extends to every in-range operand: the remaining operations (the
+// Newton fma, a*y, the residual fma, the correction fma) are IEEE operations
+// and commute with scaling by powers of two while nothing over- or
+// underflows, which the callers' range [2^-40, 2^41) guarantees; RN is
+// symmetric, so signs follow too. Mismatches counted; `first` = the lowest a
+// significand index (i >> 23) with one.
+__global__ void divcheck_kernel(unsigned long long lo, unsigned long long n, unsigned long long* bad,
+                                unsigned int* first) {
+    unsigned long long local = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const unsigned long long k = lo + i;
+        const float a = u2f(0x3f800000u | (uint32_t)(k >> 23));
+        const float b = u2f(0x3f800000u | (uint32_t)(k & 0x7fffffu));
+        float bv = b;
+        asm volatile("" : "+v"(bv));  // no constant folding of the IEEE sequence
+        if (f2u(div_inrange_(a, bv)) != f2u(a / bv)) {
+            ++local;
+            atomicMin(first, (unsigned int)(k >> 23));
+        }
+    }
+    if (local) atomicAdd(bad, local);
+}
+// fn 22: the reciprocal scales exactly: for every float b with |b| in
+// [2^-40, 2^41), rcp_newton_<1>(b) == sign(b) 2^-e rcp_newton_<1>(m) for b =
+// sign(b) m 2^e, m in [1, 2) (other patterns: not counted)
+__device__ bool rcp_scale_mismatch(uint32_t bb) {
+    const uint32_t e = (bb >> 23) & 0xffu;
+    if (e < 127u - 40u || e >= 127u + 41u) return false;
+    const float b = u2f(bb);
+    const float m = u2f(0x3f800000u | (bb & 0x7fffffu));
+    const float ym = rcp_newton_<1>(m);
+    const float want = __builtin_amdgcn_ldexpf(ym, 127 - (int)e);
+    const float y = rcp_newton_<1>(b);
+    return f2u(y) != (f2u(want) ^ (bb & 0x80000000u));
+}
+
 __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long long n,
                                  unsigned long long* bad, unsigned int* first, const float2* __restrict__ ftab) {
     unsigned long long local = 0;
@@ -2686,8 +2742,8 @@ __global__ void selfcheck_kernel(int fn, unsigned long long lo, unsigned long lo
     for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint32_t b = (uint32_t)(lo + i);
         const float x = u2f(b);
-        if (fn == 16) {  // make_frame_sc_fast == make_frame_sc<true> wherever it reports ok
-            if (frame_fast_mismatch(b)) {
+        if (fn == 16 || fn == 22) {  // 16: make_frame_sc_fast == make_frame_sc<true> wherever it reports ok
+            if (fn == 16 ? frame_fast_mismatch(b) : rcp_scale_mismatch(b)) {
                 ++local;
                 atomicMin(first, b);
             }
@@ -2749,8 +2805,33 @@ struct ChunkTiming {
     bool recorded = false;  // every event of the launch was recorded (its queueing succeeded)
 };
 
+// ipt_render's device-resident GridRenderPlane: the caller's host image is
+// the truth, the device keeps a copy of its OWNED rows (all rows unsharded,
+// the shard's tiles otherwise) across calls, and a host shadow holds those
+// rows as the previous call returned them. A call uploads only the owned row
+// runs whose host bytes differ from the shadow (none when the caller left the
+// plane alone between calls, e.g. progressive rendering), renders, and
+// downloads only the owned rows: 16 B per owned pixel per call (pixels,
+// counters, and sums / per-pixel max when the image has them) instead of the
+// whole plane both ways.
+struct ResidentPlane {
+    int W = 0, H = 0;
+    bool has_sums = false, has_pmax = false;
+    int plan[3] = {-1, -1, -1};  // (tile_rows, n_shards, shard_id) of `runs`
+    float* d_pixels = nullptr;
+    uint32_t* d_counters = nullptr;
+    float* d_sums = nullptr;
+    float* d_pmax = nullptr;
+    std::vector<std::pair<int, int>> runs;  // owned rows [y0, y1)
+    size_t owned_px = 0;
+    std::vector<uint8_t> shadow;  // per field, the owned runs' bytes as last returned
+    bool shadow_ok = false;
+    unsigned long long h2d = 0, d2h = 0;  // bytes moved by the last ipt_render
+};
+
 struct ipt_ctx {
     int device = 0;
+    ResidentPlane rp;
     int n_cu = 256;
     hipStream_t stream = nullptr;
     std::string err;
@@ -2957,6 +3038,13 @@ int settle_oldest(ipt_ctx* ctx) {
         pool_return(ctx, c);
         return fail(ctx, IPT_E_DEVICE, std::string("render launch failed: ") + hipGetErrorString(e != hipSuccess ? e : hipGetLastError()));
     }
+    // the accumulate starts after its path kernel's end (t1, the caller
+    // stream's wait): a0, recorded right behind that wait, is stamped when the
+    // wait is queued, not when it is released, so the kernel's own time is
+    // a1 - max(a0, t1)
+    float from_t1 = 0.0f;
+    if (c.a1 && hipEventElapsedTime(&from_t1, c.t1, c.a1) == hipSuccess && from_t1 >= 0.0f)
+        acc = std::min(acc, from_t1);
     if (ctx->prev.t1 && hipEventElapsedTime(&d, c.t0, ctx->prev.t1) == hipSuccess && d > 0.0f)
         path = std::max(0.0f, path - d);
     ctx->run_path_ms += path;
@@ -3500,6 +3588,8 @@ void ipt_destroy(ipt_ctx* ctx) {
         if (S.st) hipStreamDestroy(S.st);
     }
     for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);
+    for (void* b : {(void*)ctx->rp.d_pixels, (void*)ctx->rp.d_counters, (void*)ctx->rp.d_sums, (void*)ctx->rp.d_pmax})
+        if (b) hipFree(b);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -3814,31 +3904,99 @@ int ipt_render(ipt_ctx* ctx, const ipt_params* p, ipt_image* himg) {
     if (rc) return rc;
     if (!himg || !himg->pixels || !himg->counters) return fail(ctx, IPT_E_INVALID, "image pixels/counters are NULL");
     hipSetDevice(ctx->device);
-    const size_t npix = (size_t)p->width * p->height;
-    DevBuf<float> pixels, sums, pmax;
-    DevBuf<uint32_t> counters;
-    HIPCHECK(ctx, hipMalloc(&pixels.p, npix * 4));
-    HIPCHECK(ctx, hipMalloc(&counters.p, npix * 4));
-    if (himg->sums) HIPCHECK(ctx, hipMalloc(&sums.p, npix * 4));
-    if (himg->pixel_max) HIPCHECK(ctx, hipMalloc(&pmax.p, npix * 4));
-    ipt_image d{pixels.p, counters.p, sums.p, pmax.p};
+    ResidentPlane& R = ctx->rp;
+    R.h2d = R.d2h = 0;
+    const int W = p->width, H = p->height;
+    const bool has_sums = himg->sums != nullptr, has_pmax = himg->pixel_max != nullptr;
+    if (R.W != W || R.H != H || R.has_sums != has_sums || R.has_pmax != has_pmax || !R.d_pixels) {
+        for (void* b : {(void*)R.d_pixels, (void*)R.d_counters, (void*)R.d_sums, (void*)R.d_pmax})
+            if (b) hipFree(b);
+        R = ResidentPlane{};
+        const size_t npix = (size_t)W * H;
+        HIPCHECK(ctx, hipMalloc(&R.d_pixels, npix * 4));
+        HIPCHECK(ctx, hipMalloc(&R.d_counters, npix * 4));
+        if (has_sums) HIPCHECK(ctx, hipMalloc(&R.d_sums, npix * 4));
+        if (has_pmax) HIPCHECK(ctx, hipMalloc(&R.d_pmax, npix * 4));
+        R.W = W;
+        R.H = H;
+        R.has_sums = has_sums;
+        R.has_pmax = has_pmax;
+    }
+    const bool sharded = p->n_shards > 1 && p->tile_rows > 0;
+    const int plan[3] = {sharded ? p->tile_rows : 0, sharded ? p->n_shards : 1, sharded ? p->shard_id : 0};
+    if (!std::equal(plan, plan + 3, R.plan)) {
+        R.runs.clear();
+        R.owned_px = 0;
+        for (int y = 0; y < H;) {
+            if (!owned_host(p, y)) { ++y; continue; }
+            int y1 = y + 1;
+            while (y1 < H && owned_host(p, y1)) ++y1;
+            R.runs.emplace_back(y, y1);
+            R.owned_px += (size_t)(y1 - y) * W;
+            y = y1;
+        }
+        std::copy(plan, plan + 3, R.plan);
+        R.shadow_ok = false;
+    }
+    // (host field, device field) in shadow order
+    struct Field { uint8_t* h; uint8_t* d; };
+    std::vector<Field> fields = {{reinterpret_cast<uint8_t*>(himg->pixels), reinterpret_cast<uint8_t*>(R.d_pixels)},
+                                 {reinterpret_cast<uint8_t*>(himg->counters), reinterpret_cast<uint8_t*>(R.d_counters)}};
+    if (has_sums) fields.push_back({reinterpret_cast<uint8_t*>(himg->sums), reinterpret_cast<uint8_t*>(R.d_sums)});
+    if (has_pmax) fields.push_back({reinterpret_cast<uint8_t*>(himg->pixel_max), reinterpret_cast<uint8_t*>(R.d_pmax)});
+    const size_t field_bytes = R.owned_px * 4;
+    if (R.shadow.size() != fields.size() * field_bytes) {
+        R.shadow.assign(fields.size() * field_bytes, 0);
+        R.shadow_ok = false;
+    }
     hipStream_t st = ctx->stream;
-    HIPCHECK(ctx, hipMemcpyAsync(d.pixels, himg->pixels, npix * 4, hipMemcpyHostToDevice, st));
-    HIPCHECK(ctx, hipMemcpyAsync(d.counters, himg->counters, npix * 4, hipMemcpyHostToDevice, st));
-    if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(d.sums, himg->sums, npix * 4, hipMemcpyHostToDevice, st));
-    if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(d.pixel_max, himg->pixel_max, npix * 4, hipMemcpyHostToDevice, st));
+    // upload the owned runs the caller changed since the last call (all of
+    // them when the shadow is not valid)
+    for (size_t f = 0; f < fields.size(); ++f) {
+        size_t off = f * field_bytes;
+        for (const auto& r : R.runs) {
+            const size_t b0 = (size_t)r.first * W * 4, len = (size_t)(r.second - r.first) * W * 4;
+            if (!R.shadow_ok || std::memcmp(fields[f].h + b0, R.shadow.data() + off, len) != 0) {
+                HIPCHECK(ctx, hipMemcpyAsync(fields[f].d + b0, fields[f].h + b0, len, hipMemcpyHostToDevice, st));
+                R.h2d += len;
+            }
+            off += len;
+        }
+    }
+    R.shadow_ok = false;  // (valid again only once this call's rows are back)
+    ipt_image d{R.d_pixels, R.d_counters, R.d_sums, R.d_pmax};
     rc = render_chunks(ctx, p, &d, st, nullptr, nullptr);
     if (rc) {
-        (void)drain(ctx);  // no kernel or copy may still use the buffers when they are freed
+        (void)drain(ctx);  // nothing queued may still use the buffers
         (void)hipStreamSynchronize(st);
         return rc;
     }
-    HIPCHECK(ctx, hipMemcpyAsync(himg->pixels, d.pixels, npix * 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(ctx, hipMemcpyAsync(himg->counters, d.counters, npix * 4, hipMemcpyDeviceToHost, st));
-    if (d.sums) HIPCHECK(ctx, hipMemcpyAsync(himg->sums, d.sums, npix * 4, hipMemcpyDeviceToHost, st));
-    if (d.pixel_max) HIPCHECK(ctx, hipMemcpyAsync(himg->pixel_max, d.pixel_max, npix * 4, hipMemcpyDeviceToHost, st));
+    for (size_t f = 0; f < fields.size(); ++f)
+        for (const auto& r : R.runs) {
+            const size_t b0 = (size_t)r.first * W * 4, len = (size_t)(r.second - r.first) * W * 4;
+            HIPCHECK(ctx, hipMemcpyAsync(fields[f].h + b0, fields[f].d + b0, len, hipMemcpyDeviceToHost, st));
+            R.d2h += len;
+        }
     HIPCHECK(ctx, hipStreamSynchronize(st));
-    return drain(ctx);
+    rc = drain(ctx);
+    if (rc) return rc;
+    for (size_t f = 0; f < fields.size(); ++f) {
+        size_t off = f * field_bytes;
+        for (const auto& r : R.runs) {
+            const size_t b0 = (size_t)r.first * W * 4, len = (size_t)(r.second - r.first) * W * 4;
+            std::memcpy(R.shadow.data() + off, fields[f].h + b0, len);
+            off += len;
+        }
+    }
+    R.shadow_ok = true;
+    return IPT_OK;
+}
+
+int ipt_transfer_bytes(ipt_ctx* ctx, uint64_t* host_to_device, uint64_t* device_to_host) {
+    if (!ctx || !host_to_device || !device_to_host) return IPT_E_INVALID;
+    *host_to_device = ctx->rp.h2d;
+    *device_to_host = ctx->rp.d2h;
+    return IPT_OK;
 }
 
 int ipt_render_values(ipt_ctx* ctx, const ipt_params* p, float* values, uint8_t* codes) {
@@ -4013,7 +4171,8 @@ int ipt_ddf_value(ipt_ctx* ctx, int kind, const float* params, const float* dirs
 
 int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits, uint64_t* mismatches,
                        uint32_t* first_bad) {
-    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 20 || hi_bits > (1ull << 32) || lo_bits > hi_bits)
+    if (!ctx || !mismatches || !first_bad || fn < 0 || fn > 22 || hi_bits > (1ull << (fn == 21 ? 46 : 32)) ||
+        lo_bits > hi_bits)
         return IPT_E_INVALID;
     hipSetDevice(ctx->device);
     if (fn == 14 || fn == 15) {
@@ -4028,7 +4187,10 @@ int ipt_math_selfcheck(ipt_ctx* ctx, int fn, uint64_t lo_bits, uint64_t hi_bits,
     HIPCHECK(ctx, hipMemsetAsync(d_bad.p, 0, sizeof(unsigned long long), ctx->stream));
     HIPCHECK(ctx, hipMemsetAsync(d_first.p, 0xff, sizeof(unsigned int), ctx->stream));
     const unsigned long long n = hi_bits - lo_bits;
-    if (n > 0)
+    if (n > 0 && fn == 21)
+        hipLaunchKernelGGL(divcheck_kernel, dim3(ctx->n_cu * 64), dim3(256), 0, ctx->stream,
+                           (unsigned long long)lo_bits, n, d_bad.p, d_first.p);
+    else if (n > 0)
         hipLaunchKernelGGL(selfcheck_kernel, dim3(ctx->n_cu * 8), dim3(256), 0, ctx->stream, fn,
                            (unsigned long long)lo_bits, n, d_bad.p, d_first.p, ctx->d_frame_sc);
     HIPCHECK(ctx, hipGetLastError());

@@ -10,7 +10,7 @@
     (defined(IPT_BLOCK) || defined(IPT_RES_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
      defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
-     defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) ||      \
+     defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) || defined(IPT_FRAME_FB_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_CDF_POW2) || defined(IPT_PICK_INT) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG) || \
@@ -56,6 +56,10 @@
 #define IPT_FRAME_PF 3  // 3: the next step's frame-table entry gathered at the end of the step
                         // (0: in the frame pass; gathering it right after the geometry trace,
                         // or at the step's end with a predicted node, measured slower)
+#endif
+#ifndef IPT_FRAME_FB_PF
+#define IPT_FRAME_FB_PF 0  // IPT_FRAME_PF == 3: the out-of-table angle (|to.z| < 2^-8) computed in the
+                           // end-of-step prefetch too (the frame phase then reads it unconditionally)
 #endif
 #ifndef IPT_BOXDIV
 #define IPT_BOXDIV 1  // box planes' divisions without range handling (origins within 2^39)

@@ -360,13 +360,11 @@ void GpuRenderer::upload(const Scene& s) {
     check(ctx_, ipt_upload_scene(ctx_, &f.scene));
 }
 
-void GpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
-    const size_t n = plane.width * plane.height;
-    if (plane.pixels.size() != n || plane.pixel_counters.size() != n)
-        throw IptError(IPT_E_INVALID, "GridRenderPlane buffers do not match width*height");
+namespace {
+ipt_params to_params(size_t W, size_t H, const RenderParams& p) {
     ipt_params q{};
-    q.width = (int)plane.width;
-    q.height = (int)plane.height;
+    q.width = (int)W;
+    q.height = (int)H;
     q.spp = p.spp;
     q.spp_offset = p.spp_offset;
     q.n_rays = p.n_rays;
@@ -378,20 +376,54 @@ void GpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
         q.n_shards = p.n_shards;
         q.shard_id = p.shard_id;
     }
-    std::vector<uint32_t> cnt(n);
-    for (size_t i = 0; i < n; ++i) {
-        if (plane.pixel_counters[i] > 0xffffffffull - (size_t)std::max(p.spp, 0))
-            throw IptError(IPT_E_INVALID, "pixel counter would overflow 32 bits");
-        cnt[i] = (uint32_t)plane.pixel_counters[i];
+    return q;
+}
+// The plane's size_t counters as the library's 32-bit ones, and a zeroed
+// per-pixel running max (GridRenderPlane::addRay's max_value, per pixel)
+struct PlaneIo {
+    std::vector<uint32_t> cnt;
+    std::vector<float> pmax;
+    PlaneIo(const GridRenderPlane& plane, int spp) : cnt(plane.pixel_counters.size()), pmax(cnt.size(), 0.0f) {
+        for (size_t i = 0; i < cnt.size(); ++i) {
+            if (plane.pixel_counters[i] > 0xffffffffull - (size_t)std::max(spp, 0))
+                throw IptError(IPT_E_INVALID, "pixel counter would overflow 32 bits");
+            cnt[i] = (uint32_t)plane.pixel_counters[i];
+        }
     }
-    std::vector<float> pmax(n, 0.0f);
-    ipt_image img{};
-    img.pixels = plane.pixels.data();
-    img.counters = cnt.data();
-    img.pixel_max = pmax.data();
+    ipt_image image(GridRenderPlane& plane) {
+        ipt_image img{};
+        img.pixels = plane.pixels.data();
+        img.counters = cnt.data();
+        img.pixel_max = pmax.data();
+        return img;
+    }
+    void finish(GridRenderPlane& plane) const {
+        for (size_t i = 0; i < cnt.size(); ++i) plane.pixel_counters[i] = cnt[i];
+        for (float m : pmax) plane.max_value = std::max(plane.max_value, m);
+    }
+};
+void check_plane(const GridRenderPlane& plane) {
+    const size_t n = plane.width * plane.height;
+    if (plane.pixels.size() != n || plane.pixel_counters.size() != n)
+        throw IptError(IPT_E_INVALID, "GridRenderPlane buffers do not match width*height");
+}
+}  // namespace
+
+void GpuRenderer::render_image(ipt_image& img, size_t width, size_t height, const RenderParams& p) {
+    ipt_params q = to_params(width, height, p);
     check(ctx_, ipt_render(ctx_, &q, &img));
-    for (size_t i = 0; i < n; ++i) plane.pixel_counters[i] = cnt[i];
-    for (float m : pmax) plane.max_value = std::max(plane.max_value, m);
+}
+
+void GpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
+    check_plane(plane);
+    PlaneIo io(plane, p.spp);
+    ipt_image img = io.image(plane);
+    render_image(img, plane.width, plane.height, p);
+    io.finish(plane);
+}
+
+void GpuRenderer::transfer_bytes(uint64_t* host_to_device, uint64_t* device_to_host) const {
+    check(ctx_, ipt_transfer_bytes(ctx_, host_to_device, device_to_host));
 }
 
 ipt_counters GpuRenderer::counters() const {
@@ -445,10 +477,12 @@ void MultiGpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
         r_[0]->render(plane, p);
         return;
     }
-    const size_t W = plane.width, H = plane.height;
-    if (plane.pixels.size() != W * H || plane.pixel_counters.size() != W * H)
-        throw IptError(IPT_E_INVALID, "GridRenderPlane buffers do not match width*height");
-    std::vector<GridRenderPlane> part(n, plane);
+    check_plane(plane);
+    // every context renders into the caller's plane itself: ipt_render reads
+    // and writes only the context's own rows (its device keeps them between
+    // calls), so the shards share the host buffers without copies or merging
+    PlaneIo io(plane, p.spp);
+    ipt_image img = io.image(plane);
     std::vector<int> code(n, IPT_OK);
     std::vector<std::string> msg(n);
     std::vector<std::thread> th;
@@ -459,7 +493,8 @@ void MultiGpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
             q.n_shards = n;
             q.shard_id = k;
             try {
-                r_[k]->render(part[k], q);
+                ipt_image im = img;
+                r_[k]->render_image(im, plane.width, plane.height, q);
             } catch (const IptError& e) {
                 code[k] = e.code;
                 msg[k] = e.what();
@@ -471,24 +506,19 @@ void MultiGpuRenderer::render(GridRenderPlane& plane, const RenderParams& p) {
     for (auto& t : th) t.join();
     for (int k = 0; k < n; ++k)
         if (code[k] != IPT_OK) throw IptError(code[k], "shard " + std::to_string(k) + ": " + msg[k]);
-    ipt_params q{};
-    q.width = (int)W;
-    q.height = (int)H;
-    q.tile_rows = tile_rows_;
-    q.n_shards = n;
-    std::vector<uint8_t> owned(H);
-    std::vector<int32_t> cand(H);
-    int32_t n_cand = 0;
-    for (int k = 0; k < n; ++k) {
-        q.shard_id = k;
-        check(nullptr, ipt_shard_plan(&q, owned.data(), cand.data(), &n_cand));
-        for (size_t y = 0; y < H; ++y)
-            if (owned[y]) {
-                std::copy_n(part[k].pixels.begin() + y * W, W, plane.pixels.begin() + y * W);
-                std::copy_n(part[k].pixel_counters.begin() + y * W, W, plane.pixel_counters.begin() + y * W);
-            }
-        plane.max_value = std::max(plane.max_value, part[k].max_value);
+    io.finish(plane);
+}
+
+void MultiGpuRenderer::transfer_bytes(uint64_t* host_to_device, uint64_t* device_to_host) const {
+    uint64_t a = 0, b = 0;
+    for (const auto& r : r_) {
+        uint64_t x = 0, y = 0;
+        r->transfer_bytes(&x, &y);
+        a += x;
+        b += y;
     }
+    *host_to_device = a;
+    *device_to_host = b;
 }
 
 void MultiGpuRenderer::last_kernel_ms(float* path_ms, float* accumulate_ms) const {

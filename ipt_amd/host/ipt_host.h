@@ -198,6 +198,12 @@ class GpuRenderer {
     void upload(const Scene& s);
     // spp passes of render_sample accumulated into plane (bit-exact GridRenderPlane semantics)
     void render(GridRenderPlane& plane, const RenderParams& p);
+    // the same into a C-ABI image (32-bit counters); with p.n_shards > 1 only
+    // the shard's rows of it are read and written (ipt_render)
+    void render_image(ipt_image& img, size_t width, size_t height, const RenderParams& p);
+    // host <-> device bytes of the last render (ipt_transfer_bytes): the
+    // context keeps its rows of the plane on its device between calls
+    void transfer_bytes(uint64_t* host_to_device, uint64_t* device_to_host) const;
     ipt_counters counters() const;
     void last_kernel_ms(float* path_ms, float* accumulate_ms) const;
     // GridRenderPlane::smooth / computeSmoothedMax (GridRenderPlane.cpp:10-59) on the GPU
@@ -218,9 +224,10 @@ void render_samples_gpu(const Scene& scene, GridRenderPlane& plane, const Render
 // node's GPUs in one process. The reference renders with several worker
 // threads into one plane (main.cpp:256-285); here the destination rows are cut
 // into tile_rows-row tiles dealt round-robin to the contexts (ipt_shard_plan),
-// each context is driven by its own host thread on a private copy of the plane,
-// and at the end of the call the owned rows of every shard are copied into the
-// caller's plane (one owner per pixel, so nothing is summed). Each shard traces
+// each context is driven by its own host thread and renders into the caller's
+// plane directly: its device keeps the context's own rows between calls, a call
+// moves only those rows (16 B per owned pixel, ipt_render) and no other row is
+// touched (one owner per pixel, so nothing is summed or merged). Each shard traces
 // only the samples that can land in its rows, with the same (seed, pass, pixel)
 // streams: the plane is bit-identical to GpuRenderer::render's.
 class MultiGpuRenderer {
@@ -228,6 +235,8 @@ class MultiGpuRenderer {
     explicit MultiGpuRenderer(const std::vector<int>& devices, int tile_rows = 16);
     void upload(const Scene& s);
     void render(GridRenderPlane& plane, const RenderParams& p);
+    // host <-> device bytes of the last render, summed over the contexts
+    void transfer_bytes(uint64_t* host_to_device, uint64_t* device_to_host) const;
     size_t size() const { return r_.size(); }
     GpuRenderer& context(size_t k) { return *r_[k]; }
     // the slowest context's kernel time of the last render (path, accumulate ms)

@@ -106,6 +106,8 @@ int main(int argc, char** argv) {
             kernel_ms += pm + am;
         }
         const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        uint64_t h2d = 0, d2h = 0;  // the last batch's plane transfers (all contexts)
+        gpus.transfer_bytes(&h2d, &d2h);
         if (smooth > 0) gpu.smooth(plane, (size_t)smooth);
         if (glare >= 0.0 && !glare_out.empty()) {
             ipt::GridRenderPlane g(plane.width, plane.height);
@@ -126,9 +128,11 @@ int main(int argc, char** argv) {
         std::printf(
             "{\"scene\": \"%s\", \"width\": %ld, \"height\": %ld, \"spp\": %ld, \"passes\": %ld, "
             "\"n_rays\": %ld, \"depth_max\": %ld, \"devices\": %zu, \"max_value\": %.9g, \"seconds\": %.4f, "
-            "\"Mpaths_per_s\": %.3f, \"kernel_Mpaths_per_s\": %.3f}\n",
+            "\"Mpaths_per_s\": %.3f, \"kernel_Mpaths_per_s\": %.3f, \"last_batch_h2d_bytes\": %llu, "
+            "\"last_batch_d2h_bytes\": %llu}\n",
             scene_name.c_str(), width, height, spp, passes, n_rays, depth, gpus.size(), (double)plane.max_value, secs,
-            paths / secs / 1e6, kernel_ms > 0 ? paths / (kernel_ms * 1e-3) / 1e6 : 0.0);
+            paths / secs / 1e6, kernel_ms > 0 ? paths / (kernel_ms * 1e-3) / 1e6 : 0.0, (unsigned long long)h2d,
+            (unsigned long long)d2h);
     } catch (const ipt::IptError& e) {
         std::fprintf(stderr, "ipt_render: error %d: %s\n", e.code, e.what());
         return 1;

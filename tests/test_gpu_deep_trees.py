@@ -165,3 +165,30 @@ def test_coincident_spheres_tie_bit_exact(gpu_ctx, oracle, k, r, dup_stride):
     gpu_ctx.upload_scene(desc)
     gpu_ctx.reset_counters()
     _check(gpu_ctx, desc, p)
+
+
+def _high_index_spheres(n_low=32800, n_high=200):
+    """n_low tiny spheres (r = 1e-4, C3's random centres) listed before n_high
+    large ones (r = 0.05-0.09) that fill the view: camera rays hit spheres
+    whose kind 6 + index is >= 32768."""
+    desc = scenes.make_scene_spheres(n_low + n_high, seed=3)
+    sp = []
+    for i, (c, r) in enumerate(desc["spheres"]):
+        if i < n_low:
+            sp.append((c, 1e-4))
+        else:
+            sp.append(([c[0] * 0.8, c[1] * 0.8, c[2] * 0.8], 0.05 + 0.04 * ((i * 7919) % 101) / 100.0))
+    desc["spheres"] = sp
+    return desc
+
+
+def test_wide_n_rays_high_sphere_index_bit_exact(gpu_ctx, oracle):
+    """with n_rays > 255 a suspended level's meta word is ti | kind
+    << 16, and a sphere node's kind (6 + index) >= 32768 sets bit 31; the
+    decode must not sign-extend it (a negative kind reads another lane's frame
+    column). Camera rays hit spheres 32800..32999, whose children are pushed,
+    so those nodes are suspended and resumed."""
+    desc = _high_index_spheres()
+    p = capi.make_params(8, 6, 1, n_rays=260, depth_max=2)
+    ov = _check(gpu_ctx, desc, p)
+    assert (ov != 0).mean() > 0.2

@@ -138,7 +138,7 @@ def test_cli_render_matches_oracle(gpu_ctx, oracle, tmp_path):
 def test_cli_multi_context_matches_oracle(gpu_ctx, oracle, tmp_path, devices, tile):
     """The C++ N-context renderer (MultiGpuRenderer, ipt_render --devices):
     one context per listed device (all on device 0 here), rows dealt in tiles,
-    owned rows assembled after every batch; two progressive batches at a
+    each context writing its own rows of the caller's plane; two progressive batches at a
     height that is not a multiple of tile_rows x N. Pixels and counters equal
     the oracle's replay (the reference's threads, main.cpp:256-285, write one
     plane; so do the contexts here)."""
@@ -159,6 +159,11 @@ def test_cli_multi_context_matches_oracle(gpu_ctx, oracle, tmp_path, devices, ti
     assert np.array_equal(cnt, ref["counters"])
     assert np.array_equal(_bits(px), _bits(ref["pixels"]))
     assert '"devices": %d' % len(devices.split(",")) in r.stdout
+    # the contexts keep their rows on the device between batches: the last
+    # batch moved 4 B per pixel up (the zeroed per-pixel max) and 12 B down
+    import json
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (js["last_batch_h2d_bytes"], js["last_batch_d2h_bytes"]) == (4 * W * H, 12 * W * H)
 
 
 @pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs", "div_inrange_pairs", "longer_pairs",
@@ -191,6 +196,22 @@ def test_short_division_exhaustive(gpu_ctx, fn):
     (20, the hard case of Markstein's one-step theorem)."""
     bad, first = gpu_ctx.math_selfcheck(getattr(capi, fn))
     assert bad == 0, (fn, bad, hex(first))
+
+
+def test_short_division_every_significand_pair(gpu_ctx):
+    """the one-residual-step division (div_inrange_) is proved, not
+    sampled. Every pair of significands a, b in [1, 2) -- all 2^46 -- gives
+    IEEE a/b (21), and the reciprocal it starts from scales exactly over the
+    operand range [2^-40, 2^41) for all 2^32 floats (22); the other operations
+    are IEEE and commute with scaling by powers of two in that range, so the
+    division equals a/b on every in-range operand pair (ipt_math.h
+    div_inrange_). Run in 2^40-pair slices (about a second each)."""
+    bad, first = gpu_ctx.math_selfcheck(capi.SELFCHECK_RCP_SCALING)
+    assert bad == 0, ("rcp scaling", bad, hex(first))
+    step = 1 << 40
+    for lo in range(0, 1 << 46, step):
+        bad, first = gpu_ctx.math_selfcheck(capi.SELFCHECK_DIV_ALL_SIGNIFICANDS, lo, lo + step)
+        assert bad == 0, ("division", lo, bad, hex(first))
 
 
 def test_fast_frame_matches_exact(gpu_ctx):

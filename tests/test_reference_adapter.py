@@ -68,15 +68,19 @@ def test_adapter_renders_reference_plane_bit_exact(oracle, tmp_path, scene):
     mx = float(out[out.index("max_value") + 1])
     assert np.float32(mx) == ref["pixel_max"].max()
     assert int(out[out.index("uploads") + 1]) == 1  # unchanged scene: not re-uploaded
+    # device-resident plane: a later call moves 16 B per pixel (pixels,
+    # counters and per-pixel max down, the zeroed max up), not the plane twice
+    assert int(out[out.index("last_call_transfer_bytes") + 1]) == 16 * W * H
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,devices,tile", [("box", "0,0,0", 4), ("lit_corner", "0,0", 16)])
+@pytest.mark.parametrize("scene,devices,tile", [("box", "0,0,0", 4), ("lit_corner", "0,0", 16), ("box", "0", 16)])
 def test_adapter_multi_context_bit_exact(oracle, tmp_path, scene, devices, tile):
     """render_samples_multi_gpu (the adapter's N-device form for the
     reference's main, main.cpp:256-285): one context per listed device (all
     on device 0 here), tile shards rendered by one host thread each, owned
-    rows copied into the reference's GridRenderPlane. Two progressive calls at
+    rows written into the reference's GridRenderPlane (a one-entry list renders
+    on the listed device). Two progressive calls at
     a height that is not a multiple of tile x N: bit-identical to the oracle,
     each context uploaded the scene once."""
     _need_bin()
@@ -94,3 +98,6 @@ def test_adapter_multi_context_bit_exact(oracle, tmp_path, scene, devices, tile)
     out = r.stdout.split()
     assert np.float32(float(out[out.index("max_value") + 1])) == ref["pixel_max"].max()
     assert int(out[out.index("uploads") + 1]) == 1
+    # each context keeps its own rows on its device: a later call moves 16 B
+    # per pixel of the frame in all (each pixel by its one owner)
+    assert int(out[out.index("last_call_transfer_bytes") + 1]) == 16 * W * Hm
