@@ -61,6 +61,10 @@ struct KParams {
     int tile_rows, n_shards, shard_id;
     unsigned long long total_units;
     unsigned long long* unit_counter;
+    // the launch's pool-drained flag (signal memory, hipStreamWaitValue64's
+    // operand): the wave that takes the last chunk stores drain_seq there
+    unsigned long long* drained;
+    unsigned long long drain_seq;
     float* __restrict__ values;           // [spp][n_cand][W]
     uint8_t* __restrict__ codes;          // [spp][n_cand][W]
     uint8_t* __restrict__ flags;          // [H][W]
@@ -118,6 +122,11 @@ struct KParams {
     // entries, then cdf[nl] decides past the lights (cdf_p2s = 2^e)
     int cdf_p2;
     float cdf_p2s, cdf_end;
+    // the same pick on the draw's 24-bit integer g = w >> 8 (IPT_PICK_INT_CDF):
+    // floor(r 2^e) = g >> (24 - e) and r < c <=> g < ceil(c 2^24); the staged
+    // cdf then holds those integer thresholds (cdf_end_t: cdf[nl]'s)
+    int cdf_p2e;
+    uint32_t cdf_end_t;
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
@@ -198,6 +207,13 @@ __device__ __forceinline__ uint32_t sel4(uint32_t j, uint32_t x0, uint32_t x1, u
     const bool b0 = (j & 1u) != 0u, b1 = (j & 2u) != 0u;
     const uint32_t lo = b0 ? x1 : x0, hi = b0 ? x3 : x2;
     return b1 ? hi : lo;
+}
+
+// ceil(c 2^24) clamped to [0, 2^24] (0 for c <= 0 or NaN): u01(w) < c <=>
+// (w >> 8) < cdf_threshold24(c), both sides exact (host: word_threshold)
+__device__ __forceinline__ uint32_t cdf_threshold24(float c) {
+    const float x = c * 16777216.0f;
+    return !(x > 0.0f) ? 0u : (x >= 16777216.0f ? 16777216u : (uint32_t)__builtin_ceilf(x));
 }
 
 __device__ __forceinline__ void philox_fill(uint32_t& d0, uint32_t& d1, uint32_t& d2, uint32_t& d3,
@@ -1203,9 +1219,10 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
         }
     }
     if (global_lights(LMODE)) {
+        const bool int_cdf = IPT_PICK_INT_CDF && IPT_CDF_POW2 && kp.cdf_p2;
         for (int i = tid; i <= kp.n_lights; i += kBlock) {
             if (!kGridL) gl_lds[i] = kp.weights[i];
-            cdf_gl[i] = kp.cdf[i];
+            cdf_gl[i] = int_cdf ? __uint_as_float(cdf_threshold24(kp.cdf[i])) : kp.cdf[i];
         }
         if (kp.cdf_lo)
             for (int i = tid; i < kCdfBuckets; i += kBlock) cdf_lo_lds[i] = kp.cdf_lo[i];
@@ -1358,8 +1375,14 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             unsigned long long my = 0;
             if ((unsigned long long)cnt > avail) {
                 unsigned long long base = 0;
-                if (lane == __ffsll((long long)needmask) - 1)
+                if (lane == __ffsll((long long)needmask) - 1) {
                     base = atomicAdd(kp.unit_counter, (unsigned long long)kPoolChunk);
+                    // every unit handed out: release the successor launch's
+                    // gate (a plain vector store of this launch's sequence
+                    // number; every wave that gets here stores the same value)
+                    if (kp.drained && base + kPoolChunk >= kp.total_units)
+                        __hip_atomic_store(kp.drained, kp.drain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 base = __shfl(base, __ffsll((long long)needmask) - 1);
                 if ((unsigned long long)rank < avail)
                     my = pool_next + rank;
@@ -1614,7 +1637,24 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 }
                 return c;
             };
-            int c = kPickInt ? pick_w(rw) : pick_of(r);
+            // the near-uniform many-light pick on the draw's 24-bit integer
+            // (the staged cdf holds ceil(cdf 2^24), KParams::cdf_p2e)
+            auto pick_p2w = [&](uint32_t wd) {
+                const uint32_t g = wd >> 8;
+                const int ce = min((int)(g >> (24 - kp.cdf_p2e)), nl);
+                const uint32_t fa = __float_as_uint(LS.cdf(max(ce - 1, 0))), fb = __float_as_uint(LS.cdf(ce));
+                int c = (ce >= 1 && g < fa) ? ce - 1 : (g < fb ? ce : ce + 1);
+                if (c >= nl) c = g < kp.cdf_end_t ? nl : nl + 1;
+                return c;
+            };
+            constexpr bool kPickIntCdf = IPT_PICK_INT_CDF && IPT_CDF_POW2 && global_lights(LMODE);
+            auto pick_word = [&](uint32_t wd) {
+                if constexpr (kPickInt) return pick_w(wd);
+                if constexpr (kPickIntCdf)
+                    if (kp.cdf_p2) return pick_p2w(wd);
+                return pick_of(u01(wd));
+            };
+            int c = (kPickInt || kPickIntCdf) ? pick_word(rw) : pick_of(r);
             uint32_t jj = j;  // the window offset of the iteration's pick (skip-ahead: j + 3)
             if constexpr (kSkipAhead) {
                 // A light pick at a node on the lights' back side is a certain
@@ -1647,7 +1687,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     if (COUNT) { ++c_iter; ++c_lsamp; ++c_skip; }
                     k += 3;
                     jj = j + 3u;
-                    c = kPickInt ? pick_w(j == 0u ? w.a3 : w.b0) : pick_of(u01(j == 0u ? w.a3 : w.b0));  // word j + 3
+                    c = pick_word(j == 0u ? w.a3 : w.b0);  // word j + 3
                 }
             }
             pick = c;
@@ -2792,6 +2832,11 @@ struct WorkSlot {
     int cand_cap_rows = 0, cand_cap_h = 0;
     int plan[4] = {-1, -1, -1, -1};  // (H, tile_rows, n_shards, shard_id) whose rows are on the device
     unsigned long long* d_unit = nullptr;
+    // pool-drained flag in signal memory (hipExtMallocWithFlags(hipMallocSignalMemory),
+    // the memory hipStreamWaitValue64 is specified for) and the sequence
+    // number of the slot's last queued launch (the value it stores there)
+    unsigned long long* d_drained = nullptr;
+    unsigned long long seq = 0;
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr;  // after the last reader of the slot's buffers (accumulate or host copies)
     hipEvent_t path_end = nullptr;  // after its last path kernel
@@ -2858,7 +2903,7 @@ struct ipt_ctx {
     BvhNode* d_light_nodes = nullptr;
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
-    int cdf_p2 = 0;
+    int cdf_p2 = 0, cdf_p2e = 0;
     float cdf_p2s = 0.0f, cdf_end = 0.0f;
     int* d_cdf_lo = nullptr;  // cdf bucket starts (global light modes), null when a bucket is crowded
     bool any_round_light = false;
@@ -3303,7 +3348,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         // launch's pool in turn, so this wait cannot miss its value)
         if (P.used && !P.idle) {
             if (ctx->gate_on_pool)
-                HIPCHECK(ctx, hipStreamWaitValue64(S.st, P.d_unit, P.total, hipStreamWaitValueGte, ~0ull));
+                HIPCHECK(ctx, hipStreamWaitValue64(S.st, P.d_drained, P.seq, hipStreamWaitValueGte, ~0ull));
             else
                 HIPCHECK(ctx, hipStreamWaitEvent(S.st, P.path_end, 0));
         }
@@ -3346,6 +3391,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.inv_per_pass = 1.0 / (double)per_pass;
         kp.inv_w = 1.0 / (double)W;
         kp.unit_counter = S.d_unit;
+        kp.drained = ctx->gate_on_pool ? S.d_drained : nullptr;
+        kp.drain_seq = S.seq + 1;
         kp.values = S.d_values;
         kp.codes = S.d_codes;
         kp.flags = S.d_flags;
@@ -3390,6 +3437,8 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cdf_p2 = ctx->cdf_p2;
         kp.cdf_p2s = ctx->cdf_p2s;
         kp.cdf_end = ctx->cdf_end;
+        kp.cdf_p2e = ctx->cdf_p2e;
+        kp.cdf_end_t = (uint32_t)(word_threshold(ctx->cdf_end) >> 8);
         kp.cdf_lo = ctx->d_cdf_lo;
         kp.lgrid = ctx->d_lgrid;
         kp.lax = reinterpret_cast<const float4*>(ctx->d_lax);
@@ -3433,6 +3482,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         rc = susp <= 4 ? launch_path<4>(ctx, kp, ss, count) : launch_path<8>(ctx, kp, ss, count);
         if (rc) return rc;
         S.total = kp.total_units;
+        S.seq = kp.drain_seq;
         HIPCHECK(ctx, hipEventRecord(tm.t1, ss));
         HIPCHECK(ctx, hipEventRecord(S.path_end, ss));
         if (host_values) {  // [spp][H][W] (whole frames: per_pass == W * H)
@@ -3530,9 +3580,10 @@ int ipt_create(int hip_device, ipt_ctx** out) {
     }
     if (const char* e = std::getenv("IPT_TEST_CHUNK_UNITS")) ctx->chunk_cap_test = (size_t)std::atoll(e);  // tests
     {
-        // (measured: hipStreamWaitValue64 on hipMalloc memory releases the
-        // waiting stream ~0.6 us after a kernel's atomicAdd reaches the value,
-        // scripts/probes/waitvalue_probe.hip). A tool that serialises the
+        // (round 4 measured hipStreamWaitValue64 on hipMalloc memory releasing
+        // the waiting stream ~0.6 us after a kernel's atomicAdd reached the
+        // value, scripts/probes/waitvalue_probe.hip; since round 6 the wait is
+        // on a signal-memory flag, the memory the API specifies). A tool that serialises the
         // dispatches to collect counters or traces (rocprofv3 --pmc / --att,
         // which export ROCPROF_COUNTER_COLLECTION / ROCPROF_ADVANCED_THREAD_TRACE
         // to the profiled process) never released such a wait queued behind a
@@ -3543,7 +3594,10 @@ int ipt_create(int hip_device, ipt_ctx** out) {
             const char* v = std::getenv(n);
             return v && *v && std::strcmp(v, "0") != 0 && strcasecmp(v, "false") != 0 && strcasecmp(v, "off") != 0;
         };
-        const bool serialising_tool = env_on("ROCPROF_COUNTER_COLLECTION") || env_on("ROCPROF_ADVANCED_THREAD_TRACE");
+        // (IPT_FORCE_POOL_GATE=1: keep the pool gate under such a tool --
+        // diagnostics of that hang only)
+        const bool serialising_tool = (env_on("ROCPROF_COUNTER_COLLECTION") || env_on("ROCPROF_ADVANCED_THREAD_TRACE")) &&
+                                      !env_on("IPT_FORCE_POOL_GATE");
         int wv = 0;
         ctx->gate_on_pool = !env_on("IPT_NO_TAIL_OVERLAP") && !serialising_tool &&
                             hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, hip_device) ==
@@ -3559,7 +3613,25 @@ int ipt_create(int hip_device, ipt_ctx** out) {
             ipt_destroy(ctx);
             return fail(nullptr, IPT_E_DEVICE, "work-slot stream / event / counter creation failed");
         }
+        // the pool-drained flag: signal memory, set to 0 by a stream write
+        // (without it -- allocation refused -- launches gate on events)
+        if (ctx->gate_on_pool) {
+            void* sig = nullptr;
+            if (hipExtMallocWithFlags(&sig, sizeof(unsigned long long), hipMallocSignalMemory) != hipSuccess ||
+                hipStreamWriteValue64(S.st, sig, 0ull, 0) != hipSuccess || hipStreamSynchronize(S.st) != hipSuccess) {
+                if (sig) hipFree(sig);
+                sig = nullptr;
+                ctx->gate_on_pool = false;
+                (void)hipGetLastError();
+            }
+            S.d_drained = reinterpret_cast<unsigned long long*>(sig);
+        }
     }
+    if (!ctx->gate_on_pool)
+        for (WorkSlot& S : ctx->slot) {
+            if (S.d_drained) hipFree(S.d_drained);
+            S.d_drained = nullptr;
+        }
     if (hipMalloc(&ctx->d_counters, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps)) != hipSuccess ||
         hipMalloc(&ctx->d_wall, sizeof(Frame) * 5) != hipSuccess) {
         ipt_destroy(ctx);
@@ -3580,7 +3652,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     for (void* b : bufs)
         if (b) hipFree(b);
     for (WorkSlot& S : ctx->slot) {
-        void* sb[] = {S.d_values, S.d_codes, S.d_rg, S.d_flags, S.d_cand_rows, S.d_cand_of_row, S.d_unit};
+        void* sb[] = {S.d_values, S.d_codes, S.d_rg, S.d_flags, S.d_cand_rows, S.d_cand_of_row, S.d_unit, S.d_drained};
         for (void* b : sb)
             if (b) hipFree(b);
         if (S.done) hipEventDestroy(S.done);
@@ -3817,6 +3889,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         if (ok) {
             ctx->cdf_p2 = 1;
             ctx->cdf_p2s = std::ldexp(1.0f, e);
+            ctx->cdf_p2e = e;
             ctx->cdf_end = cdf[nl];
         }
     }

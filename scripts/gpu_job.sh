@@ -14,6 +14,7 @@
 #   profile=CFG,CFG       rocprof stats + PMC traffic passes + bench lines (TAG env)
 #   phases=CFG,CFG        IPT_PROF / IPT_STAMP builds' phase profiles (scripts/prof_phases.sh first)
 #   ubench                VALU / packed-f32 issue microbenchmark (scripts/ubench_valu)
+#   gate[=LIBS]           the tail-overlap gate under rocprofv3 (scripts/gpu_gate_trace.sh; FORCE env)
 #
 # usage (gpurun): /usr/local/graft/bin/gpurun --timeout 900 -- 'bash scripts/gpu_job.sh tests=async bench=c2'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -70,6 +71,8 @@ step() {
       TAG=$TAG CFGS="${v//,/ }" bash scripts/gpu_profile.sh ;;
     phases)
       CONFIGS="${v//,/ }" bash scripts/gpu_prof_phases.sh ;;
+    gate)
+      LIBS="${v//,/ }" FORCE=${FORCE:-0} bash scripts/gpu_gate_trace.sh ;;
     ubench)
       timeout -k 10 300 ./scripts/ubench_valu > gpurun_out/ubench_valu.jsonl && cat gpurun_out/ubench_valu.jsonl ;;
     *) echo "unknown step $s"; return 2 ;;
