@@ -84,6 +84,10 @@ struct KParams {
     float grid_g1[3];                     // g0 + (float)n * h, the grid's far corner (host-computed)
     int grid_n[3];
     const int* __restrict__ grid_start;   // [cells + 1]
+    // IPT_GRID_LDS: grid_start packed for LDS staging -- [grid_packed_nb] u32
+    // bases of 8-entry blocks, then [cells + 1] u8 offsets from them
+    const int* __restrict__ grid_packed;
+    int grid_packed_words, grid_packed_nb;
     const GridCell* __restrict__ grid_cells;  // [cells] range + first three items (IPT_GRID_INLINE)
     const BvhSphere* __restrict__ grid_items;
     // the same items packed for the pipelined walk (IPT_GRID_C4): centre and
@@ -596,10 +600,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 // utilisation instead of once per lane per item slot. Same cells, same tests
 // (sphere_t on the same operands), same exit decisions: the (t, index) minimum
 // does not depend on the order of the tests. Every lane of the wave calls it.
+// grid_start[lin] from global memory, or (IPT_GRID_LDS) from the packed copy
+// staged in LDS (gl): an 8-entry block's base plus the entry's byte offset
+__device__ __forceinline__ int grid_start_at(const KParams& kp, const int* gl, int lin) {
+    if constexpr (IPT_GRID_LDS != 0) {
+        const uint8_t* off = reinterpret_cast<const uint8_t*>(gl + kp.grid_packed_nb);
+        return gl[lin >> 3] + (int)off[lin];
+    }
+    return kp.grid_start[lin];
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool walking, vec3 o, vec3 d, int& cell,
                                                       vec3& tmx, float& best, int& bidx, int budget,
-                                                      unsigned long long* slots, int lane,
+                                                      unsigned long long* slots, int lane, const int* gl,
                                                       uint32_t& c_nodes, uint32_t& c_tests IPT_DIAG_PARAMS) {
     const vec3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     auto lin_of = [&](int c) {
@@ -609,8 +623,8 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
     int s0 = 0, s1 = 0;
     if (act) {
         const int lin = lin_of(cell);
-        s0 = kp.grid_start[lin];
-        s1 = kp.grid_start[lin + 1];
+        s0 = grid_start_at(kp, gl, lin);
+        s1 = grid_start_at(kp, gl, lin + 1);
     }
     for (int it = 0;; ++it) {
         // (after IPT_GRID_WAVE_FLOOR_IT iterations the wave stops once fewer than
@@ -650,8 +664,8 @@ __device__ __forceinline__ void sphere_grid_walk_wave(const KParams& kp, bool wa
             ncell = nvalid ? ncell : -1;
             // (no next cell: cell 0's range, unused)
             const int nlin = nvalid ? lin_of(ncell) : 0;
-            n0 = kp.grid_start[nlin];
-            n1 = kp.grid_start[nlin + 1];
+            n0 = grid_start_at(kp, gl, nlin);
+            n1 = grid_start_at(kp, gl, nlin + 1);
         }
         const int cnt = act ? s1 - s0 : 0;
         if (COUNT && act) {
@@ -1013,7 +1027,8 @@ __host__ __device__ constexpr bool resumable_geom(int geom);
 // progressive calls 0.964 -> 0.985 of one call); C2 keeps 256 (its frame
 // columns' ds_read2st64 stride, -1.2 % at 64).
 __host__ __device__ constexpr int block_of(int lmode, int geom) {
-    return (lmode == 9 || lmode == 10) ? kLatticeBlock : (resumable_geom(geom) ? IPT_RES_BLOCK : kBlock);
+    return (lmode == 9 || lmode == 10) ? kLatticeBlock
+                                       : (resumable_geom(geom) ? (IPT_GRID_LDS ? IPT_GRID_LDS_BLOCK : IPT_RES_BLOCK) : kBlock);
 }
 // the wave-spread grid walk's per-lane LDS (IPT_GRID_WAVE): an 8-byte slot
 __host__ __device__ constexpr int walk_lds_words(int lmode, int geom) {
@@ -1192,7 +1207,10 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
     float* stk = lds + walk_lds_words(LMODE, GEOM);           // [MAXSUSP][F][kBlock]
     constexpr int kFrameStride = frame_stride(LMODE, GEOM);
     float* lfr = stk + MAXSUSP * kStackFields * kBlock;       // [12][kFrameStride] lane + wall frames
-    LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride);
+    // IPT_GRID_LDS: the packed grid ranges after the frames
+    constexpr bool kGridLds = IPT_GRID_LDS && resumable_geom(GEOM);
+    int* grid_lds = reinterpret_cast<int*>(lfr + 12 * kFrameStride);
+    LightDev* lights_lds = reinterpret_cast<LightDev*>(lfr + 12 * kFrameStride + (kGridLds ? kp.grid_packed_words : 0));
     float* weights_lds = reinterpret_cast<float*>(lights_lds) + kLdsLights * kLightWords;
     float* cdf_lds = weights_lds + (kLdsLights + 1);
     // kLightsGlobal: [weights | cdf | light BVH nodes] after the frames
@@ -1209,6 +1227,8 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
     const int wave = tid >> 6;
     const bool sharded = !(kp.n_shards <= 1 || kp.tile_rows <= 0);
     if (tid < 60) lfr[(tid % 12) * kFrameStride + kBlock + tid / 12] = reinterpret_cast<const float*>(kp.wall_frames)[tid];
+    if (kGridLds)
+        for (int i = tid; i < kp.grid_packed_words; i += kBlock) grid_lds[i] = kp.grid_packed[i];
     if (LMODE == kLightsLds) {
         const float* src = reinterpret_cast<const float*>(kp.lights);
         float* dst = reinterpret_cast<float*>(lights_lds);
@@ -2279,7 +2299,7 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                                                   wslots + (tid & ~63), wown + (tid & ~63), lane, c_nodes, c_tests);
                 else
                     sphere_grid_walk_wave<COUNT>(kg, tracing, xo, xrd, xi, xtm, xbest, xbidx, IPT_GRID_BUDGET,
-                                                 wslots + (tid & ~63), lane, c_nodes, c_tests IPT_DIAG_ARGS);
+                                                 wslots + (tid & ~63), lane, grid_lds, c_nodes, c_tests IPT_DIAG_ARGS);
             }
             if (tracing && xi < 0) {
                 tracing = false;
@@ -2897,6 +2917,8 @@ struct ipt_ctx {
     int n_grid = 0;
     size_t grid_n_items = 0;
     int* d_grid_start = nullptr;
+    int* d_grid_packed = nullptr;  // IPT_GRID_LDS (KParams::grid_packed)
+    int grid_packed_words = 0, grid_packed_nb = 0;
     BvhSphere* d_grid_items = nullptr;
     float4* d_grid_c4 = nullptr;  // [items] centre/radius, then [items] original indices
     GridCell* d_grid_cells = nullptr;  // 64-byte cell records (IPT_GRID_INLINE)
@@ -3199,6 +3221,7 @@ size_t path_lds_bytes(const KParams& kp) {
     constexpr int kBlock = block_of(LMODE, GEOM);
     const size_t cells = (size_t)kp.lg_nu * kp.lg_nv;
     return ((size_t)MAXSUSP * kStackFields * kBlock + scene_lds_words(LMODE, GEOM) +
+            ((IPT_GRID_LDS && resumable_geom(GEOM)) ? (size_t)kp.grid_packed_words : 0) +
             (LMODE == kLightsGlobal ? global_light_lds_words(kp.n_lights, kp.lnodes_lds ? kp.n_light_nodes : 0) : 0) +
             (grid_lights(LMODE) ? global_light_lds_words(kp.n_lights, 0, true) +
                                       (lax_in_lds(LMODE) ? ((cells + 3) & ~(size_t)3) + 12 * (size_t)kp.n_lights : cells)
@@ -3209,6 +3232,8 @@ size_t path_lds_bytes(const KParams& kp) {
 template <int MAXSUSP, bool COUNT, int LMODE, int GEOM>
 int launch_path4(ipt_ctx* ctx, const KParams& kp, hipStream_t st) {
     constexpr int kBlock = block_of(LMODE, GEOM);
+    if (IPT_GRID_LDS && resumable_geom(GEOM) && kp.n_grid > 0 && !kp.grid_packed)
+        return fail(ctx, IPT_E_UNSUPPORTED, "IPT_GRID_LDS build: the grid's ranges do not pack into bytes");
     const size_t lds = path_lds_bytes<MAXSUSP, LMODE, GEOM>(kp);
     const void* fn = (const void*)path_kernel<MAXSUSP, COUNT, LMODE, GEOM>;
     HIPCHECK(ctx, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -3421,6 +3446,9 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         }
         kp.grid_m = ctx->grid.m;
         kp.grid_start = ctx->d_grid_start;
+        kp.grid_packed = ctx->d_grid_packed;
+        kp.grid_packed_words = ctx->grid_packed_words;
+        kp.grid_packed_nb = ctx->grid_packed_nb;
         kp.grid_items = ctx->d_grid_items;
         kp.grid_c4 = ctx->d_grid_c4;
         kp.grid_idx = ctx->d_grid_c4 ? reinterpret_cast<const int*>(ctx->d_grid_c4 + ctx->grid_n_items) : nullptr;
@@ -3648,7 +3676,8 @@ void ipt_destroy(ipt_ctx* ctx) {
     (void)drain(ctx);  // nothing queued may still use the buffers
     void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_lax, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
                     ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
-                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_frame_sc};
+                    ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_frame_sc,
+                    ctx->d_grid_packed};
     for (void* b : bufs)
         if (b) hipFree(b);
     for (WorkSlot& S : ctx->slot) {
@@ -3804,7 +3833,7 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         if (count) HIPCHECK(ctx, hipMemcpy(buf.p, src, sizeof(T) * count, hipMemcpyHostToDevice));
         return IPT_OK;
     };
-    DevBuf<int> n_grid_start, n_lgrid, n_cdf_lo;
+    DevBuf<int> n_grid_start, n_lgrid, n_cdf_lo, n_grid_packed;
     DevBuf<LightAx> n_lax;
     DevBuf<BvhSphere> n_grid_items, n_bvh_prims;
     DevBuf<float4> n_grid_c4;
@@ -3817,6 +3846,25 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     int rc = IPT_OK;
     if (use_grid && !rc) rc = upload(n_grid_start, grid.start.data(), grid.start.size());
     if (use_grid && !rc) rc = upload(n_grid_items, grid.items.data(), grid.items.size());
+    // IPT_GRID_LDS: grid.start as 8-entry block bases + byte offsets (every
+    // offset must fit a byte, else the instance is refused at render time)
+    std::vector<int> packed;
+    int packed_nb = 0;
+    if (IPT_GRID_LDS && use_grid) {
+        const size_t ne = grid.start.size();
+        packed_nb = (int)((ne + 7) / 8);
+        packed.assign((size_t)packed_nb + (ne + 3) / 4, 0);
+        uint8_t* off = reinterpret_cast<uint8_t*>(packed.data() + packed_nb);
+        bool fits = true;
+        for (size_t e = 0; e < ne; ++e) {
+            if (e % 8 == 0) packed[e / 8] = grid.start[e];
+            const int d = grid.start[e] - packed[e / 8];
+            fits &= d >= 0 && d <= 255;
+            off[e] = (uint8_t)d;
+        }
+        if (!fits) packed.clear();
+        if (!packed.empty() && !rc) rc = upload(n_grid_packed, packed.data(), packed.size());
+    }
     if (IPT_GRID_C4 && use_grid && !rc) {
         const size_t ni = grid.items.size();
         std::vector<float4> c4(ni + (ni + 3) / 4);
@@ -3848,10 +3896,13 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (rc) return rc;  // the temporaries free themselves; the context keeps no scene
     void* old[] = {ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_spheres, ctx->d_bvh_nodes, ctx->d_bvh_prims,
                    ctx->d_light_nodes, ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_wall, ctx->d_lgrid, ctx->d_lax,
-                   ctx->d_cdf_lo};
+                   ctx->d_cdf_lo, ctx->d_grid_packed};
     for (void* b : old)
         if (b) hipFree(b);
     ctx->d_grid_start = n_grid_start.release();
+    ctx->d_grid_packed = n_grid_packed.release();
+    ctx->grid_packed_words = (int)packed.size();
+    ctx->grid_packed_nb = packed_nb;
     ctx->d_grid_items = n_grid_items.release();
     ctx->d_grid_c4 = n_grid_c4.release();
     ctx->d_grid_cells = n_grid_cells.release();

@@ -8,7 +8,7 @@
 
 #if !defined(IPT_AB_BUILD) &&                                                                           \
     (defined(IPT_BLOCK) || defined(IPT_RES_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
-     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
+     defined(IPT_GRID_BUDGET) || defined(IPT_GRID_LDS) || defined(IPT_GRID_LDS_BLOCK) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) || defined(IPT_FRAME_FB_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_CDF_POW2) || defined(IPT_PICK_INT) || defined(IPT_PICK_INT_CDF) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
@@ -142,6 +142,13 @@
 static_assert(IPT_GRID_WAVE != 2 || IPT_GRID_C4, "IPT_GRID_WAVE=2 needs IPT_GRID_C4 (kp.grid_c4 / grid_idx)");
 
 // ---- walk budgets and acceleration-structure parameters
+#ifndef IPT_GRID_LDS
+#define IPT_GRID_LDS 0  // sphere-list instances: the grid's cell ranges packed and staged in LDS, one
+                        // IPT_GRID_LDS_BLOCK-thread workgroup per CU sharing them
+#endif
+#ifndef IPT_GRID_LDS_BLOCK
+#define IPT_GRID_LDS_BLOCK 896
+#endif
 #ifndef IPT_GRID_INLINE
 #define IPT_GRID_INLINE 0  // 1: the grid walk over 64-byte cell records (range + first 3 items inline): C3 -9 %
 #endif

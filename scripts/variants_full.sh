@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p ipt_amd/lib/abl
 while [ $# -ge 2 ]; do
   n=$1; f=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -fno-slp-vectorize -mllvm -structurizecfg-skip-uniform-regions=true -mllvm -structurizecfg-relaxed-uniform-regions=true \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-memory-clause \
     -Wno-unused-value -DIPT_AB_BUILD $f -o ipt_amd/lib/abl/libipt_$n.so ipt_amd/csrc/ipt_kernels.hip ipt_amd/csrc/ipt_post.hip &
   pids="$pids $!"
 done

@@ -60,3 +60,19 @@ def test_shard_plan_partitions_rows():
                     assert iy in cand
             assert list(cand) == sorted(cand)
         assert (owners == 1).all(), n_shards
+
+
+def test_product_build_keeps_uniform_regions_structurized():
+    """Round 6: with -mllvm -structurizecfg-skip-uniform-regions (rounds 4-5)
+    the compiler built IPT_FLAG_COUNTERS instances that rendered different
+    trees from the same source as the product instances (a code motion of the
+    frame fallback; gpurun_out/diverge.log: 10 of 2048 box samples, samples
+    whose camera ray misses everything given non-zero values), and the same
+    source without the option is bit-exact in both. The
+    product library, the A/B and the diagnostic builds leave it out."""
+    import __graft_entry__ as ge
+    from pathlib import Path
+    assert not any("structurizecfg" in f for f in ge.HIPCC_FLAGS)
+    root = Path(ge.__file__).resolve().parent
+    for sh in ("variants.sh", "variants_full.sh", "regs.sh", "prof_phases.sh"):
+        assert "structurizecfg" not in (root / "scripts" / sh).read_text(), sh

@@ -192,3 +192,32 @@ def test_chunked_call_under_counter_collection(tmp_path):
                         sys.executable, str(probe)], capture_output=True, text=True, env=env, timeout=200)
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     assert "bit-exact" in r.stdout
+
+
+def test_chunked_call_under_pool_gate_traced(tmp_path):
+    """A synchronous call split into several launches with the pool gate on
+    (each launch's stream waits on its predecessor's pool-drained flag,
+    hipStreamWaitValue64 on signal memory) completes bit-exact under a
+    trace-only rocprofv3 run (--kernel-trace: no dispatch serialisation, so the
+    gate stays on), and the trace shows the runtime's wait kernel
+    (__amd_rocclr_streamOpsWait): the stream wait runs as a polling kernel,
+    which is why a dispatch-serialising tool deadlocks it."""
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not Path(prof).exists():
+        pytest.skip("rocprofv3 not installed")
+    probe = Path(__file__).resolve().parent / "chunked_probe.py"
+    env = dict(__import__("os").environ, IPT_TEST_CHUNK_UNITS="3000", TMPDIR="/tmp")
+    r = subprocess.run(["timeout", "-s", "KILL", "150", prof, "--kernel-trace", "--stats", "--output-format", "csv",
+                        "-d", str(tmp_path / "prof"), "-o", "run", "--", sys.executable, str(probe)],
+                       capture_output=True, text=True, env=env, timeout=200)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "bit-exact" in r.stdout
+    stats = list((tmp_path / "prof").rglob("*kernel_stats.csv"))
+    assert stats, "no kernel stats written"
+    names = stats[0].read_text()
+    assert "path_kernel" in names and "streamOpsWait" in names

@@ -58,13 +58,21 @@ def test_image_bit_exact_box(gpu_ctx, oracle):
 
 
 def test_counters_match_oracle(gpu_ctx, oracle):
+    """The counting instance (IPT_FLAG_COUNTERS, 128 VGPRs) renders the same
+    samples as the product instance and the oracle, and counts the oracle's
+    events. (Round 5's frame-fallback code motion, built with
+    -structurizecfg-skip-uniform-regions, broke exactly this: 10 of these 2048
+    samples and traced_rays 338 341 vs 338 173)"""
     desc = scenes.make_scene_box()
     p = capi.make_params(32, 32, 2, flags=capi.IPT_FLAG_COUNTERS)
     gpu_ctx.upload_scene(desc)
     gpu_ctx.reset_counters()
-    gpu_ctx.render_values(p)
+    cv, cc = gpu_ctx.render_values(p)
     g = gpu_ctx.counters()
-    _, _, o = ob.render_values(desc, capi.make_params(32, 32, 2), 0, with_counters=True)
+    pv, pc = gpu_ctx.render_values(capi.make_params(32, 32, 2))
+    ov, oc, o = ob.render_values(desc, capi.make_params(32, 32, 2), 0, with_counters=True)
+    assert np.array_equal(_bits(cv), _bits(pv)) and np.array_equal(cc, pc)
+    assert np.array_equal(_bits(cv), _bits(ov)) and np.array_equal(cc, oc)
     for k in ("paths", "traced_rays", "surface_hits", "light_hits", "expanded_nodes",
               "iterations", "light_samples", "skipped", "light_traces", "drifted"):
         assert g[k] == o[k], (k, g[k], o[k])
@@ -160,10 +168,12 @@ def test_cli_multi_context_matches_oracle(gpu_ctx, oracle, tmp_path, devices, ti
     assert np.array_equal(_bits(px), _bits(ref["pixels"]))
     assert '"devices": %d' % len(devices.split(",")) in r.stdout
     # the contexts keep their rows on the device between batches: the last
-    # batch moved 4 B per pixel up (the zeroed per-pixel max) and 12 B down
+    # batch moved 12 B per pixel down and at most 4 B up (the zeroed per-pixel
+    # max, for the row runs whose previous maxima were not all zero)
     import json
     js = json.loads(r.stdout.strip().splitlines()[-1])
-    assert (js["last_batch_h2d_bytes"], js["last_batch_d2h_bytes"]) == (4 * W * H, 12 * W * H)
+    assert js["last_batch_d2h_bytes"] == 12 * W * H
+    assert js["last_batch_h2d_bytes"] <= 4 * W * H
 
 
 @pytest.mark.parametrize("fn", ["acos_f64_f32", "sqrtf", "div_pairs", "div_inrange_pairs", "longer_pairs",

@@ -68,9 +68,10 @@ def test_adapter_renders_reference_plane_bit_exact(oracle, tmp_path, scene):
     mx = float(out[out.index("max_value") + 1])
     assert np.float32(mx) == ref["pixel_max"].max()
     assert int(out[out.index("uploads") + 1]) == 1  # unchanged scene: not re-uploaded
-    # device-resident plane: a later call moves 16 B per pixel (pixels,
-    # counters and per-pixel max down, the zeroed max up), not the plane twice
-    assert int(out[out.index("last_call_transfer_bytes") + 1]) == 16 * W * H
+    # device-resident plane: a later call moves 12 B per pixel down (pixels,
+    # counters, per-pixel max) and at most 4 B up (the zeroed max, for row runs
+    # whose previous maxima were not all zero), not the whole plane both ways
+    assert 12 * W * H <= int(out[out.index("last_call_transfer_bytes") + 1]) <= 16 * W * H
 
 
 @pytest.mark.gpu
@@ -98,6 +99,6 @@ def test_adapter_multi_context_bit_exact(oracle, tmp_path, scene, devices, tile)
     out = r.stdout.split()
     assert np.float32(float(out[out.index("max_value") + 1])) == ref["pixel_max"].max()
     assert int(out[out.index("uploads") + 1]) == 1
-    # each context keeps its own rows on its device: a later call moves 16 B
-    # per pixel of the frame in all (each pixel by its one owner)
-    assert int(out[out.index("last_call_transfer_bytes") + 1]) == 16 * W * Hm
+    # each context keeps its own rows on its device: a later call moves at
+    # most 16 B per pixel of the frame in all (each pixel by its one owner)
+    assert 12 * W * Hm <= int(out[out.index("last_call_transfer_bytes") + 1]) <= 16 * W * Hm
