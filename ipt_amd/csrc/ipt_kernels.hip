@@ -2412,6 +2412,9 @@ struct AParams {
     uint32_t* counters;
     float* sums;
     float* pixel_max;
+    // [2]: the launch's first block start and last block end on the 100 MHz
+    // wall clock (atomic min / max; the host presets them), for its duration
+    unsigned long long* clk;
 };
 
 __device__ __forceinline__ void add_ray(float v, float& p, uint32_t& c, float& s, float& m) {
@@ -2422,12 +2425,17 @@ __device__ __forceinline__ void add_ray(float v, float& p, uint32_t& c, float& s
     if (p > m) m = p;
 }
 
+__device__ __forceinline__ void accumulate_pixel(const AParams& ap, int xi, int yi);
 __global__ __launch_bounds__(256) void accumulate_kernel(AParams ap) {
     const int xi = blockIdx.x * blockDim.x + threadIdx.x;
     const int yi = blockIdx.y;
-    if (xi >= ap.W) return;
-    if (!(ap.n_shards <= 1 || ap.tile_rows <= 0 || ((yi / ap.tile_rows) % ap.n_shards) == ap.shard_id))
-        return;
+    if (threadIdx.x == 0) atomicMin(&ap.clk[0], (unsigned long long)wall_clock64());
+    if (xi < ap.W && (ap.n_shards <= 1 || ap.tile_rows <= 0 || ((yi / ap.tile_rows) % ap.n_shards) == ap.shard_id))
+        accumulate_pixel(ap, xi, yi);
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&ap.clk[1], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void accumulate_pixel(const AParams& ap, int xi, int yi) {
     const size_t d = (size_t)yi * ap.W + xi;
     float p = ap.pixels[d];
     uint32_t c = ap.counters[d];
@@ -2867,8 +2875,10 @@ struct WorkSlot {
 struct ChunkTiming {
     hipEvent_t t0 = nullptr, t1 = nullptr;  // raygen start, path-kernel end (slot stream)
     hipEvent_t a0 = nullptr, a1 = nullptr;  // accumulate (caller stream; null without an image)
+    int clk = -1;           // the accumulate's wall-clock pair in ctx->d_clk (ring entry)
     bool recorded = false;  // every event of the launch was recorded (its queueing succeeded)
 };
+constexpr int kClkRing = 32;  // > the launches settle_oldest lets queue up (8) plus the last settled one
 
 // ipt_render's device-resident GridRenderPlane: the caller's host image is
 // the truth, the device keeps a copy of its OWNED rows (all rows unsharded,
@@ -2955,6 +2965,13 @@ struct ipt_ctx {
     ChunkTiming prev{};  // the last processed launch (its path-end event bounds the next one's start)
     std::vector<hipEvent_t> ev_pool;
     float run_path_ms = 0.0f, run_acc_ms = 0.0f;
+    // accumulate_kernel's start / end wall-clock stamps, a ring of kClkRing
+    // pairs (HIP events on the caller's stream are stamped when its wait for
+    // the path kernel is queued, not when it is released)
+    unsigned long long* d_clk = nullptr;
+    unsigned long long* d_clk_dummy = nullptr;  // (2 words: stamps of an untimed launch)
+    unsigned next_clk = 0;
+    double clk_khz = 100000.0;
     unsigned long long* d_counters = nullptr;
     float* d_cos_a = nullptr;   // CosineDdf tables (cos_table_kernel): r 64 MiB,
                                 // (cos phi, sin phi) 128 MiB
@@ -3105,13 +3122,14 @@ int settle_oldest(ipt_ctx* ctx) {
         pool_return(ctx, c);
         return fail(ctx, IPT_E_DEVICE, std::string("render launch failed: ") + hipGetErrorString(e != hipSuccess ? e : hipGetLastError()));
     }
-    // the accumulate starts after its path kernel's end (t1, the caller
-    // stream's wait): a0, recorded right behind that wait, is stamped when the
-    // wait is queued, not when it is released, so the kernel's own time is
-    // a1 - max(a0, t1)
-    float from_t1 = 0.0f;
-    if (c.a1 && hipEventElapsedTime(&from_t1, c.t1, c.a1) == hipSuccess && from_t1 >= 0.0f)
-        acc = std::min(acc, from_t1);
+    // the accumulate kernel's own duration from its wall-clock stamps (the
+    // events bracket the caller stream's wait for the path kernel as well)
+    if (c.a1 && c.clk >= 0 && ctx->d_clk) {
+        unsigned long long h[2] = {~0ull, 0ull};
+        if (hipMemcpy(h, ctx->d_clk + 2 * c.clk, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[0] != ~0ull &&
+            h[1] >= h[0])
+            acc = (float)((double)(h[1] - h[0]) / ctx->clk_khz);
+    }
     if (ctx->prev.t1 && hipEventElapsedTime(&d, c.t0, ctx->prev.t1) == hipSuccess && d > 0.0f)
         path = std::max(0.0f, path - d);
     ctx->run_path_ms += path;
@@ -3525,6 +3543,13 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
             // after this launch's path kernel
             HIPCHECK(ctx, hipStreamWaitEvent(st, tm.t1, 0));
             HIPCHECK(ctx, hipEventRecord(tm.a0, st));
+            unsigned long long* clk = nullptr;
+            if (ctx->d_clk) {
+                tmq.clk = (int)(ctx->next_clk++ % kClkRing);
+                clk = ctx->d_clk + 2 * tmq.clk;
+                HIPCHECK(ctx, hipMemsetAsync(clk, 0xff, sizeof(unsigned long long), st));
+                HIPCHECK(ctx, hipMemsetAsync(clk + 1, 0, sizeof(unsigned long long), st));
+            }
             AParams ap{};
             ap.W = W;
             ap.H = H;
@@ -3541,6 +3566,7 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
             ap.counters = img->counters;
             ap.sums = img->sums;
             ap.pixel_max = img->pixel_max;
+            ap.clk = clk ? clk : ctx->d_clk_dummy;
             dim3 grid((W + 255) / 256, H), block(256);
             hipLaunchKernelGGL(accumulate_kernel, grid, block, 0, st, ap);
             HIPCHECK(ctx, hipGetLastError());
@@ -3666,6 +3692,17 @@ int ipt_create(int hip_device, ipt_ctx** out) {
         return fail(nullptr, IPT_E_OOM, "hipMalloc failed");
     }
     hipMemset(ctx->d_counters, 0, sizeof(unsigned long long) * (kNumCounters + 2 * kProfPhases + kStamps));
+    if (hipMalloc(&ctx->d_clk, sizeof(unsigned long long) * 2 * (kClkRing + 1)) != hipSuccess) {
+        ipt_destroy(ctx);
+        return fail(nullptr, IPT_E_OOM, "hipMalloc failed");
+    }
+    ctx->d_clk_dummy = ctx->d_clk + 2 * kClkRing;
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, hip_device) == hipSuccess && khz > 0)
+            ctx->clk_khz = (double)khz;
+        (void)hipGetLastError();
+    }
     *out = ctx;
     return IPT_OK;
 }
@@ -3675,7 +3712,7 @@ void ipt_destroy(ipt_ctx* ctx) {
     hipSetDevice(ctx->device);
     (void)drain(ctx);  // nothing queued may still use the buffers
     void* bufs[] = {ctx->d_cdf_lo, ctx->d_lgrid, ctx->d_lax, ctx->d_bvh_nodes, ctx->d_bvh_prims, ctx->d_light_nodes, ctx->d_lights, ctx->d_weights, ctx->d_cdf, ctx->d_wall, ctx->d_spheres,
-                    ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b,
+                    ctx->d_counters, ctx->d_cos_a, ctx->d_cos_b, ctx->d_clk,
                     ctx->d_grid_start, ctx->d_grid_items, ctx->d_grid_c4, ctx->d_grid_cells, ctx->d_frame_sc,
                     ctx->d_grid_packed};
     for (void* b : bufs)
