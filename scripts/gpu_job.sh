@@ -14,6 +14,7 @@
 #   profile=CFG,CFG       rocprof stats + PMC traffic passes + bench lines (TAG env)
 #   phases=CFG,CFG        IPT_PROF / IPT_STAMP builds' phase profiles (scripts/prof_phases.sh first)
 #   ubench                VALU / packed-f32 issue microbenchmark (scripts/ubench_valu)
+#   gather                dependent-gather latency by table size (scripts/ubench_gather)
 #   gate[=LIBS]           the tail-overlap gate under rocprofv3 (scripts/gpu_gate_trace.sh; FORCE env)
 #
 # usage (gpurun): /usr/local/graft/bin/gpurun --timeout 900 -- 'bash scripts/gpu_job.sh tests=async bench=c2'
@@ -71,6 +72,8 @@ step() {
       TAG=$TAG CFGS="${v//,/ }" bash scripts/gpu_profile.sh ;;
     phases)
       CONFIGS="${v//,/ }" bash scripts/gpu_prof_phases.sh ;;
+    gather)
+      timeout -k 10 300 ./scripts/ubench_gather > gpurun_out/ubench_gather.jsonl && cat gpurun_out/ubench_gather.jsonl ;;
     gate)
       LIBS="${v//,/ }" FORCE=${FORCE:-0} bash scripts/gpu_gate_trace.sh ;;
     ubench)
