@@ -124,7 +124,7 @@ struct KParams {
     // |cdf[i] - (i+1) 2^-e| < 2^-e/2 for every light i and a non-decreasing
     // cdf (host-checked): the pick is floor(r 2^e) - 1, + 0 or + 1 by two cdf
     // entries, then cdf[nl] decides past the lights (cdf_p2s = 2^e)
-    int cdf_p2;
+    int cdf_p2;  // 1: near-uniform as above; 2: every threshold exact (KParams::cdf_p2e)
     float cdf_p2s, cdf_end;
     // the same pick on the draw's 24-bit integer g = w >> 8 (IPT_PICK_INT_CDF):
     // floor(r 2^e) = g >> (24 - e) and r < c <=> g < ceil(c 2^24); the staged
@@ -1662,6 +1662,11 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             auto pick_p2w = [&](uint32_t wd) {
                 const uint32_t g = wd >> 8;
                 const int ce = min((int)(g >> (24 - kp.cdf_p2e)), nl);
+                if (kp.cdf_p2 == 2) {
+                    // every light's threshold is exactly (i+1) 2^(24-e)
+                    // (host-checked): the first i with g < T[i] is ce itself
+                    return ce < nl ? ce : (g < kp.cdf_end_t ? nl : nl + 1);
+                }
                 const uint32_t fa = __float_as_uint(LS.cdf(max(ce - 1, 0))), fb = __float_as_uint(LS.cdf(ce));
                 int c = (ce >= 1 && g < fa) ? ce - 1 : (g < fb ? ce : ce + 1);
                 if (c >= nl) c = g < kp.cdf_end_t ? nl : nl + 1;
@@ -3976,6 +3981,15 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
         for (int i = 0; ok && i < nl; ++i) ok = std::fabs((double)cdf[i] - (double)(i + 1) * w) < 0.25 * w;
         if (ok) {
             ctx->cdf_p2 = 1;
+            // exactly uniform on the draw's 24-bit integer: every light's
+            // ceil(cdf[i] 2^24) is (i+1) 2^(24-e) (C5's 256 equal emitters),
+            // so the integer pick reads no cdf entry at all (KParams::cdf_p2 2)
+            if (IPT_PICK_INT_CDF && IPT_CDF_EXACT && e <= 24) {
+                bool exact = true;
+                for (int i = 0; exact && i < nl; ++i)
+                    exact = (word_threshold(cdf[i]) >> 8) == ((unsigned long long)(i + 1) << (24 - e));
+                if (exact) ctx->cdf_p2 = 2;
+            }
             ctx->cdf_p2s = std::ldexp(1.0f, e);
             ctx->cdf_p2e = e;
             ctx->cdf_end = cdf[nl];

@@ -11,7 +11,7 @@
      defined(IPT_GRID_BUDGET) || defined(IPT_GRID_LDS) || defined(IPT_GRID_LDS_BLOCK) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
      defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_FRAME_PF) || defined(IPT_FRAME_FB_PF) ||      \
-     defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_CDF_POW2) || defined(IPT_PICK_INT) || defined(IPT_PICK_INT_CDF) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
+     defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_CDF_POW2) || defined(IPT_PICK_INT) || defined(IPT_PICK_INT_CDF) || defined(IPT_CDF_EXACT) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG) || \
      defined(IPT_COSB_TAB) || defined(IPT_SKIP_AHEAD) || defined(IPT_PRE_SKIP))
@@ -105,6 +105,9 @@
 #endif
 #ifndef IPT_PICK_INT_CDF
 #define IPT_PICK_INT_CDF 1  // the near-uniform many-light pick (IPT_CDF_POW2) on the draw's 24-bit integer
+#endif
+#ifndef IPT_CDF_EXACT
+#define IPT_CDF_EXACT 1  // ... and when every light's integer threshold is exactly (i+1) 2^(24-e): no cdf read
 #endif
 #ifndef IPT_CDF_POW2
 #define IPT_CDF_POW2 1  // many lights whose cdf is within 2^-e/2 of (i+1) 2^-e: the pick from floor(r 2^e)
