@@ -6,14 +6,11 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${TAG:-latest}
 for c in ${CFGS:-c2 c3 c5}; do
-  # the kernel-trace pass runs the bench's own queued steps (tracing does not
-  # serialise dispatches; the accumulate then overlaps the next launch as in
-  # the bench line); the counter passes run --sync: counter collection
-  # serialises the dispatches, and a launch gated on its predecessor's pool
-  # (a polling wait kernel) then never starts
+  # (--sync: counter collection serialises the dispatches, and a launch gated
+  # on its predecessor's pool -- a polling wait kernel, DESIGN.md 4.7 -- then
+  # never starts; bench.py runs synchronous steps under any rocprofv3 anyway)
   B="python3 bench.py --config $c --steps 2 --warmup 1 --cpu-seconds 0 --no-counters --sync"
-  BQ="python3 bench.py --config $c --steps 2 --warmup 1 --cpu-seconds 0 --no-counters"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_${c}_stats -o run -- $BQ > gpurun_out/${T}_${c}_stats.json 2> gpurun_out/${T}_${c}_stats.err || { echo "$c stats failed"; tail gpurun_out/${T}_${c}_stats.err; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_${c}_stats -o run -- $B > gpurun_out/${T}_${c}_stats.json 2> gpurun_out/${T}_${c}_stats.err || { echo "$c stats failed"; tail gpurun_out/${T}_${c}_stats.err; exit 1; }
   for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
               "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_32B_sum GRBM_GUI_ACTIVE" \
               "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_DRAM_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"; do
