@@ -131,6 +131,12 @@ struct KParams {
     // cdf then holds those integer thresholds (cdf_end_t: cdf[nl]'s)
     int cdf_p2e;
     uint32_t cdf_end_t;
+    // IPT_LPF_CALC: the lattice lights' sample fields are a formula of the
+    // light index i (host-checked for every light): P.x = lc_x0 + (float)(i &
+    // (2^lc_shift - 1)) * lc_dx, P.y = lc_y0 + (float)(i >> lc_shift) * lc_dy,
+    // x[XA] = lc_ax, y[YA] = lc_ay (C5's 16 x 16 split light, built that way)
+    int lpf_calc, lc_shift;
+    float lc_x0, lc_y0, lc_dx, lc_dy, lc_ax, lc_ay;
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
@@ -1556,11 +1562,20 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                 if constexpr (grid_lights(LMODE) && IPT_LPF && IPT_LIGHT_AX_REC) {
                     // the compact record's first 16 bytes: P.xy, x[XA], y[YA]
                     // (P.z, n.z: the lattice plane; lattice lights are diamonds)
-                    const int li = 3 * ((ran && pick >= 0 && pick < nl) ? pick : 0);
-                    const float4 a = kLaxLds ? lax_lds[li] : kp.lax[li];
-                    lpP = v3(a.x, a.y, kp.lg_pn);
-                    lpx = a.z;
-                    lpy = a.w;
+                    const int pk = (ran && pick >= 0 && pick < nl) ? pick : 0;
+                    if (IPT_LPF_CALC && kp.lpf_calc) {
+                        // the same floats from the lattice's formula (no LDS
+                        // read on the pick -> light sample chain)
+                        lpP = v3(kp.lc_x0 + (float)(pk & ((1 << kp.lc_shift) - 1)) * kp.lc_dx,
+                                 kp.lc_y0 + (float)(pk >> kp.lc_shift) * kp.lc_dy, kp.lg_pn);
+                        lpx = kp.lc_ax;
+                        lpy = kp.lc_ay;
+                    } else {
+                        const float4 a = kLaxLds ? lax_lds[3 * pk] : kp.lax[3 * pk];
+                        lpP = v3(a.x, a.y, kp.lg_pn);
+                        lpx = a.z;
+                        lpy = a.w;
+                    }
                     lpn = kp.lg_nn;
                     lptype = 0;
                 } else if constexpr (grid_lights(LMODE) && IPT_LPF) {
@@ -2941,6 +2956,8 @@ struct ipt_ctx {
     int n_light_nodes = 0;
     int cdf_bsearch = 0;
     int cdf_p2 = 0, cdf_p2e = 0;
+    int lpf_calc = 0, lc_shift = 0;  // KParams::lpf_calc
+    float lc[6] = {0, 0, 0, 0, 0, 0};
     float cdf_p2s = 0.0f, cdf_end = 0.0f;
     int* d_cdf_lo = nullptr;  // cdf bucket starts (global light modes), null when a bucket is crowded
     bool any_round_light = false;
@@ -3489,6 +3506,14 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.cdf_p2s = ctx->cdf_p2s;
         kp.cdf_end = ctx->cdf_end;
         kp.cdf_p2e = ctx->cdf_p2e;
+        kp.lpf_calc = ctx->lpf_calc;
+        kp.lc_shift = ctx->lc_shift;
+        kp.lc_x0 = ctx->lc[0];
+        kp.lc_y0 = ctx->lc[1];
+        kp.lc_dx = ctx->lc[2];
+        kp.lc_dy = ctx->lc[3];
+        kp.lc_ax = ctx->lc[4];
+        kp.lc_ay = ctx->lc[5];
         kp.cdf_end_t = (uint32_t)(word_threshold(ctx->cdf_end) >> 8);
         kp.cdf_lo = ctx->d_cdf_lo;
         kp.lgrid = ctx->d_lgrid;
@@ -3927,6 +3952,38 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     if (lg.pattern)
         for (int i = 0; i < nl; ++i) laxr.push_back(light_ax_record(L[i], lg.pattern, wts[i]));
     if (lg.pattern && !rc) rc = upload(n_lax, laxr.data(), laxr.size());
+    // IPT_LPF_CALC: is every lattice light's sample record the formula of its
+    // index (a power-of-two row length, one origin, one pitch per axis)? The
+    // exact float operations of the kernel are replayed here for every light.
+    int lpf_calc = 0, lc_shift = 0;
+    float lcv[6] = {0, 0, 0, 0, 0, 0};
+    if (IPT_LPF_CALC && lg.pattern && nl >= 2) {
+        int row = 1;
+        while (row < nl && laxr[row].py == laxr[0].py) ++row;
+        const bool p2 = row >= 2 && (row & (row - 1)) == 0 && nl % row == 0;
+        if (p2) {
+            lc_shift = 0;
+            while ((1 << lc_shift) < row) ++lc_shift;
+            const float cand[2] = {laxr[0].xa, laxr[0].ya};
+            for (int cx = 0; cx < 2 && !lpf_calc; ++cx)
+                for (int cy = 0; cy < 2 && !lpf_calc; ++cy) {
+                    const float x0 = laxr[0].px, y0 = laxr[0].py, dx = cand[cx], dy = cand[cy];
+                    bool ok = true;
+                    for (int i = 0; ok && i < nl; ++i) {
+                        volatile float fx = (float)(i & (row - 1)) * dx;  // (no contraction, as the kernel)
+                        volatile float fy = (float)(i >> lc_shift) * dy;
+                        const float px = x0 + fx, py = y0 + fy;
+                        ok = f2u(px) == f2u(laxr[i].px) && f2u(py) == f2u(laxr[i].py) &&
+                             f2u(laxr[i].xa) == f2u(laxr[0].xa) && f2u(laxr[i].ya) == f2u(laxr[0].ya);
+                    }
+                    if (ok) {
+                        lpf_calc = 1;
+                        lcv[0] = x0; lcv[1] = y0; lcv[2] = dx; lcv[3] = dy;
+                        lcv[4] = laxr[0].xa; lcv[5] = laxr[0].ya;
+                    }
+                }
+        }
+    }
     if (use_cdf_lo && !rc) rc = upload(n_cdf_lo, cdf_lo.data(), cdf_lo.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_nodes, bnodes.data(), bnodes.size());
     if (!bnodes.empty() && !rc) rc = upload(n_bvh_prims, bprims.data(), bprims.size());
@@ -3962,6 +4019,9 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->d_lgrid = n_lgrid.release();
     ctx->d_lax = n_lax.release();
     ctx->d_cdf_lo = n_cdf_lo.release();
+    ctx->lpf_calc = lpf_calc;
+    ctx->lc_shift = lc_shift;
+    std::copy(lcv, lcv + 6, ctx->lc);
     lg.cells.clear();
     ctx->lgrid = lg;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;
