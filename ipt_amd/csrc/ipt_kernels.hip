@@ -137,6 +137,12 @@ struct KParams {
     // x[XA] = lc_ax, y[YA] = lc_ay (C5's 16 x 16 split light, built that way)
     int lpf_calc, lc_shift;
     float lc_x0, lc_y0, lc_dx, lc_dy, lc_ax, lc_ay;
+    // IPT_LTR_CALC (with lpf_calc): every lattice light's inverse entries,
+    // area and power are the same (lc_ix .. lc_spow), so a light test reads
+    // only the light's weight; lg_ident 1 / 2: cell (i, j) holds light
+    // i + nu j / j + nv i (every cell, host-checked), no cell read
+    int ltr_calc, lg_ident;
+    float lc_ix, lc_iy, lc_area, lc_spow;
     const int* __restrict__ cdf_lo;       // [kCdfBuckets] or null: first c with cdf[c] > b/256
     double inv_per_pass, inv_w;           // 1/(n_cand*W), 1/W (exact 32-bit unit decomposition)
     uint32_t per_pass32;                  // n_cand*W (< 2^32)
@@ -2157,7 +2163,14 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     // fields light_trace_ax / light_pdf_ax read (ipt_path.h LightAx)
                     constexpr int XA = lattice_a10(LMODE) ? 1 : 0, YA = 1 - XA;
                     float4 a, b, c;
-                    if constexpr (kLaxLds) {
+                    if (IPT_LTR_CALC && kp.ltr_calc) {
+                        // the record's floats from the lattice's formulas; only
+                        // the weight is per light
+                        a = make_float4(kp.lc_x0 + (float)(l & ((1 << kp.lc_shift) - 1)) * kp.lc_dx,
+                                        kp.lc_y0 + (float)(l >> kp.lc_shift) * kp.lc_dy, kp.lc_ax, kp.lc_ay);
+                        b = make_float4(kp.lc_ix, kp.lc_iy, kp.lc_area, kp.lc_spow);
+                        c = make_float4(kLaxLds ? lax_lds[3 * l + 2].x : kp.lax[3 * l + 2].x, 0.0f, 0.0f, 0.0f);
+                    } else if constexpr (kLaxLds) {
                         a = lax_lds[3 * l]; b = lax_lds[3 * l + 1]; c = lax_lds[3 * l + 2];
                     } else {
                         const float4* r = kp.lax + 3 * l;
@@ -2212,7 +2225,10 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
                     const int j0 = (int)floorf(v - e), j1 = (int)floorf(v + e);
                     const int* cells = reinterpret_cast<const int*>(lnodes_lds);
                     auto cell = [&](int i, int j) {
-                        return (i >= 0 && i < kp.lg_nu && j >= 0 && j < kp.lg_nv) ? cells[i + kp.lg_nu * j] : -1;
+                        const bool in = i >= 0 && i < kp.lg_nu && j >= 0 && j < kp.lg_nv;
+                        if (IPT_LTR_CALC && kp.lg_ident)
+                            return in ? (kp.lg_ident == 1 ? i + kp.lg_nu * j : j + kp.lg_nv * i) : -1;
+                        return in ? cells[i + kp.lg_nu * j] : -1;
                     };
                     cand[0] = cell(i0, j0);
                     cand[1] = i1 != i0 ? cell(i1, j0) : -1;
@@ -2957,7 +2973,8 @@ struct ipt_ctx {
     int cdf_bsearch = 0;
     int cdf_p2 = 0, cdf_p2e = 0;
     int lpf_calc = 0, lc_shift = 0;  // KParams::lpf_calc
-    float lc[6] = {0, 0, 0, 0, 0, 0};
+    int ltr_calc = 0, lg_ident = 0;  // KParams::ltr_calc, lg_ident
+    float lc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float cdf_p2s = 0.0f, cdf_end = 0.0f;
     int* d_cdf_lo = nullptr;  // cdf bucket starts (global light modes), null when a bucket is crowded
     bool any_round_light = false;
@@ -3514,6 +3531,12 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.lc_dy = ctx->lc[3];
         kp.lc_ax = ctx->lc[4];
         kp.lc_ay = ctx->lc[5];
+        kp.ltr_calc = ctx->ltr_calc;
+        kp.lg_ident = ctx->lg_ident;
+        kp.lc_ix = ctx->lc[6];
+        kp.lc_iy = ctx->lc[7];
+        kp.lc_area = ctx->lc[8];
+        kp.lc_spow = ctx->lc[9];
         kp.cdf_end_t = (uint32_t)(word_threshold(ctx->cdf_end) >> 8);
         kp.cdf_lo = ctx->d_cdf_lo;
         kp.lgrid = ctx->d_lgrid;
@@ -3955,8 +3978,8 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     // IPT_LPF_CALC: is every lattice light's sample record the formula of its
     // index (a power-of-two row length, one origin, one pitch per axis)? The
     // exact float operations of the kernel are replayed here for every light.
-    int lpf_calc = 0, lc_shift = 0;
-    float lcv[6] = {0, 0, 0, 0, 0, 0};
+    int lpf_calc = 0, lc_shift = 0, ltr_calc = 0, lg_ident = 0;
+    float lcv[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (IPT_LPF_CALC && lg.pattern && nl >= 2) {
         int row = 1;
         while (row < nl && laxr[row].py == laxr[0].py) ++row;
@@ -3982,6 +4005,25 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
                         lcv[4] = laxr[0].xa; lcv[5] = laxr[0].ya;
                     }
                 }
+        }
+        // the light tests' records: the rest uniform, the cells an index formula
+        if (IPT_LTR_CALC && lpf_calc) {
+            bool same = true;
+            for (int i = 1; same && i < nl; ++i)
+                same = f2u(laxr[i].ix) == f2u(laxr[0].ix) && f2u(laxr[i].iy) == f2u(laxr[0].iy) &&
+                       f2u(laxr[i].area) == f2u(laxr[0].area) && f2u(laxr[i].spow) == f2u(laxr[0].spow);
+            if (same) {
+                ltr_calc = 1;
+                lcv[6] = laxr[0].ix; lcv[7] = laxr[0].iy; lcv[8] = laxr[0].area; lcv[9] = laxr[0].spow;
+            }
+            bool id1 = (int)lg.cells.size() == lg.nu * lg.nv, id2 = id1;
+            for (int j = 0; (id1 || id2) && j < lg.nv; ++j)
+                for (int i = 0; i < lg.nu; ++i) {
+                    const int c = lg.cells[i + lg.nu * j];
+                    id1 = id1 && c == i + lg.nu * j;
+                    id2 = id2 && c == j + lg.nv * i;
+                }
+            lg_ident = id1 ? 1 : (id2 ? 2 : 0);
         }
     }
     if (use_cdf_lo && !rc) rc = upload(n_cdf_lo, cdf_lo.data(), cdf_lo.size());
@@ -4021,7 +4063,9 @@ int ipt_upload_scene(ipt_ctx* ctx, const ipt_scene* s) {
     ctx->d_cdf_lo = n_cdf_lo.release();
     ctx->lpf_calc = lpf_calc;
     ctx->lc_shift = lc_shift;
-    std::copy(lcv, lcv + 6, ctx->lc);
+    ctx->ltr_calc = ltr_calc;
+    ctx->lg_ident = lg_ident;
+    std::copy(lcv, lcv + 10, ctx->lc);
     lg.cells.clear();
     ctx->lgrid = lg;
     ctx->cdf_bsearch = cdf_mono ? 1 : 0;

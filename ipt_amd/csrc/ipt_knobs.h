@@ -10,7 +10,7 @@
     (defined(IPT_BLOCK) || defined(IPT_RES_BLOCK) || defined(IPT_RESUME) || defined(IPT_RESUME_LIGHTS) || defined(IPT_SPHERE_GRID) || \
      defined(IPT_GRID_BUDGET) || defined(IPT_GRID_LDS) || defined(IPT_GRID_LDS_BLOCK) || defined(IPT_GRID_INLINE) || defined(IPT_GRID_C4) || defined(IPT_GRID_ITEMS) || defined(IPT_GRID_PIPE) || defined(IPT_GRID_WAVE) || defined(IPT_GRID_WAVE_PIPE) || defined(IPT_GRID_WAVE_UNC) || defined(IPT_GRID_WAVE_FLOOR) || defined(IPT_GRID_WAVE_FLOOR_IT) ||                   \
      defined(IPT_WALK_BUDGET) || defined(IPT_LWALK_BUDGET) || defined(IPT_WAVES_PER_SIMD) ||           \
-     defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_LPF_CALC) || defined(IPT_FRAME_PF) || defined(IPT_FRAME_FB_PF) ||      \
+     defined(IPT_RES_WAVES) || defined(IPT_RES_HOLD) || defined(IPT_LIGHT_HOLD) || defined(IPT_RESL_WAVES) || defined(IPT_BOXDIV) || defined(IPT_LPF) || defined(IPT_LPF_CALC) || defined(IPT_LTR_CALC) || defined(IPT_FRAME_PF) || defined(IPT_FRAME_FB_PF) ||      \
      defined(IPT_LIGHT_INR) || defined(IPT_LIGHT_AXIS) || defined(IPT_LIGHT_GRID) || defined(IPT_CDF_LO) || defined(IPT_CDF_POW2) || defined(IPT_PICK_INT) || defined(IPT_PICK_INT_CDF) || defined(IPT_CDF_EXACT) || defined(IPT_LIGHT_AX_REC) || defined(IPT_LAX_LDS) || \
      defined(IPT_RAYGEN) || defined(IPT_FRAME_TAB) || defined(IPT_FRAME_TAB_LISTS) || defined(IPT_C2_ONLY) || defined(IPT_C2_LMODE) ||  \
      defined(IPT_BVH_LEAF) || defined(IPT_LBVH_LEAF) || defined(IPT_GRID_CELLS_PER_SPHERE) || defined(IPT_GRID_SPHERE_REG) || \
@@ -90,6 +90,9 @@
 #endif
 #ifndef IPT_LPF_CALC
 #define IPT_LPF_CALC 1  // ... computed from the light index where every light matches the lattice formula
+#endif
+#ifndef IPT_LTR_CALC
+#define IPT_LTR_CALC 1  // ... and the light tests' records and cell lookup too (only the weight is read)
 #endif
 #ifndef IPT_LIGHT_AX_REC
 #define IPT_LIGHT_AX_REC 1  // lattice lights read from 48-byte compact records (three 16-byte loads)
