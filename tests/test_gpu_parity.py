@@ -635,3 +635,51 @@ def test_near_uniform_cdf_pick(gpu_ctx, oracle, case):
     assert np.array_equal(_bits(vals), _bits(ov))
     for k in ("iterations", "light_samples", "skipped", "light_hits"):
         assert g[k] == o[k], (case, k, g[k], o[k])
+
+
+@pytest.mark.parametrize("n_shards", [1, 3])
+def test_resident_render_sees_caller_changes(oracle, n_shards):
+    """ipt_render keeps the rows a context accumulates on its device between
+    calls (ABI 5). The caller's host plane stays the truth: rows the caller
+    changes between calls are uploaded again, rows it leaves alone are not,
+    and the result equals a fresh context's render of the same plane. Shards
+    (one context each) share one host plane and touch only their own rows."""
+    desc = scenes.make_scene_box()
+    W, H, tile = 40, 37, 4
+    ctxs = [capi.Context(0) for _ in range(n_shards)]
+    fresh = [capi.Context(0) for _ in range(n_shards)]
+    try:
+        for c in ctxs + fresh:
+            c.upload_scene(desc)
+
+        def params(spp, off, k):
+            return capi.make_params(W, H, spp, spp_offset=off, tile_rows=tile if n_shards > 1 else 0,
+                                    n_shards=n_shards, shard_id=k)
+
+        img = {k: np.zeros(W * H, dt) for k, dt in (("pixels", np.float32), ("counters", np.uint32),
+                                                    ("pixel_max", np.float32))}
+        for k, c in enumerate(ctxs):
+            c.render(params(2, 0, k), img)
+        # an untouched plane: the next call uploads nothing but the zeroed max
+        img["pixel_max"][:] = 0
+        before = {k: v.copy() for k, v in img.items()}
+        for k, c in enumerate(ctxs):
+            c.render(params(1, 2, k), img)
+            h2d, d2h = c.transfer_bytes()
+            assert h2d <= 4 * W * H and d2h > 0
+        # the caller edits the plane (a row of pixels, some counters), then renders on
+        img["pixels"][5 * W:6 * W] = 0.25
+        img["counters"][17 * W + 3:17 * W + 9] += 7
+        img["pixel_max"][:] = 0
+        edited = {k: v.copy() for k, v in img.items()}
+        for k, c in enumerate(ctxs):
+            c.render(params(2, 3, k), img)
+        ref = {k: v.copy() for k, v in edited.items()}
+        for k, c in enumerate(fresh):
+            c.render(params(2, 3, k), ref)
+        for k in img:
+            assert np.array_equal(_bits(img[k]), _bits(ref[k])), k
+        assert not np.array_equal(_bits(before["pixels"]), _bits(img["pixels"]))
+    finally:
+        for c in ctxs + fresh:
+            c.close()
