@@ -9,7 +9,11 @@
 //                  previous stamp; read their SHARES (the stamps' waits forbid
 //                  overlaps the real kernel has);
 //   -DIPT_MARK=1 / -DIPT_MARK_PHASES=1  asm-listing builds: a ;@STAMP / ;@PHASE
-//                  comment at each hook (per-segment instruction counts).
+//                  comment at each hook (per-segment instruction counts);
+//   -DIPT_RAYLOG=1 every raylog_every-th finished sphere-list trace of the
+//                  resumable instances (origin, direction, nearest t, hit) into
+//                  a device buffer (scripts/probes/walk_split.hip, the split
+//                  traversal measurement).
 // None of them changes a result.
 #pragma once
 
@@ -25,9 +29,20 @@
 #ifndef IPT_MARK_PHASES
 #define IPT_MARK_PHASES 0
 #endif
-#if (IPT_PROF || IPT_STAMP || IPT_MARK || IPT_MARK_PHASES) && !defined(IPT_DIAGNOSTIC_BUILD)
-#error "IPT_PROF / IPT_STAMP / IPT_MARK* are diagnostic: build with -DIPT_DIAGNOSTIC_BUILD, outside ipt_amd/lib"
+#ifndef IPT_RAYLOG
+#define IPT_RAYLOG 0
 #endif
+#if (IPT_PROF || IPT_STAMP || IPT_MARK || IPT_MARK_PHASES || IPT_RAYLOG) && !defined(IPT_DIAGNOSTIC_BUILD)
+#error "IPT_PROF / IPT_STAMP / IPT_MARK* / IPT_RAYLOG are diagnostic: build with -DIPT_DIAGNOSTIC_BUILD, outside ipt_amd/lib"
+#endif
+
+// IPT_RAYLOG's record: a traced ray and the walk's result (t bits, and the
+// hit: sphere index >= 0, or -2 - box plane)
+struct RayLogRec {
+    float o[3], t;
+    float d[3];
+    int hit;
+};
 
 constexpr int kProfPhases = 12;
 constexpr int kStamps = 12;

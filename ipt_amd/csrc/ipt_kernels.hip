@@ -65,6 +65,12 @@ struct KParams {
     // operand): the wave that takes the last chunk stores drain_seq there
     unsigned long long* drained;
     unsigned long long drain_seq;
+#if IPT_RAYLOG
+    RayLogRec* raylog;               // [raylog_cap]
+    unsigned long long* raylog_n;    // finished traces seen
+    unsigned long long raylog_cap;
+    unsigned raylog_every;
+#endif
     float* __restrict__ values;           // [spp][n_cand][W]
     uint8_t* __restrict__ codes;          // [spp][n_cand][W]
     uint8_t* __restrict__ flags;          // [H][W]
@@ -2340,6 +2346,17 @@ __global__ __launch_bounds__(block_of(LMODE, GEOM), waves_per_simd(GEOM, LMODE))
             if (tracing && xi < 0) {
                 tracing = false;
                 if (IPT_GRID_WAVE != 2 && xbidx >= 0) xbidx = grid_item_index(kg, xbidx);  // item position -> original index
+#if IPT_RAYLOG
+                if (!COUNT && kp.raylog) {
+                    const unsigned long long k = atomicAdd(kp.raylog_n, 1ull);
+                    if (k % kp.raylog_every == 0 && k / kp.raylog_every < kp.raylog_cap) {
+                        RayLogRec r;
+                        r.o[0] = xo.x; r.o[1] = xo.y; r.o[2] = xo.z; r.t = xbest;
+                        r.d[0] = xrd.x; r.d[1] = xrd.y; r.d[2] = xrd.z; r.hit = xbidx;
+                        kp.raylog[k / kp.raylog_every] = r;
+                    }
+                }
+#endif
                 resolve(true, xbest, xbidx >= 0 ? 6 + xbidx : -2 - xbidx, xo, xrd, xis_iter ? tdepth + 1 : 0, xis_iter,
                         xmult, xhas_li, xli_y, xli_pow);
             }
@@ -2908,6 +2925,14 @@ struct WorkSlot {
     bool used = false;
     bool idle = true;  // its last launch is known complete (a drain since): nothing to wait for
 };
+#if IPT_RAYLOG
+// IPT_RAYLOG's buffer (scripts/probes/walk_split.hip arms it)
+static RayLogRec* g_raylog = nullptr;
+static unsigned long long* g_raylog_n = nullptr;
+static unsigned long long g_raylog_cap = 0;
+static unsigned g_raylog_every = 1;
+#endif
+
 struct ChunkTiming {
     hipEvent_t t0 = nullptr, t1 = nullptr;  // raygen start, path-kernel end (slot stream)
     hipEvent_t a0 = nullptr, a1 = nullptr;  // accumulate (caller stream; null without an image)
@@ -3474,6 +3499,12 @@ int render_chunks(ipt_ctx* ctx, const ipt_params* p, ipt_image* img, hipStream_t
         kp.inv_w = 1.0 / (double)W;
         kp.unit_counter = S.d_unit;
         kp.drained = ctx->gate_on_pool ? S.d_drained : nullptr;
+#if IPT_RAYLOG
+        kp.raylog = g_raylog;
+        kp.raylog_n = g_raylog_n;
+        kp.raylog_cap = g_raylog_cap;
+        kp.raylog_every = g_raylog_every;
+#endif
         kp.drain_seq = S.seq + 1;
         kp.values = S.d_values;
         kp.codes = S.d_codes;
