@@ -256,7 +256,10 @@ def main():
     share = os.environ.get("IPT_BENCH_SHARE_GPU") == "1"
     if share:
         local_rank = 0
-    if world > 1:
+    # IPT_BENCH_FORCE_DIST=1 (test only): the process group, frame-end gather
+    # and collectives of the N>1 path also at world 1, so the RCCL branch runs
+    # on a one-GPU box (tests/test_gpu_rccl_branch.py)
+    if world > 1 or os.environ.get("IPT_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
 
         if share:
@@ -356,7 +359,7 @@ def main():
     value = total_paths / elapsed / 1e6
 
     verify = None
-    if args.verify and world > 1 and rank == 0:
+    if args.verify and dist and rank == 0:
         whole = torch.zeros_like(state)
         for step in range(args.steps):
             render(params(spp_step, step * spp_step, shard=0, n_shards=1), whole)
@@ -558,7 +561,7 @@ def main():
                                 if cnt else None),
             "mean_pixel": mean_pixel,
         }
-        if world > 1:
+        if dist:
             out["ranks"] = ranks
             if ranks:
                 pm = [r["path_ms"] for r in ranks]
