@@ -104,7 +104,7 @@ BAD = [
     (dict(depth_max=65), capi.IPT_E_INVALID),
     (dict(n_rays=-1), capi.IPT_E_UNSUPPORTED),
     (dict(n_rays=65536), capi.IPT_E_UNSUPPORTED),
-    (dict(n_rays=300, depth_max=10), capi.IPT_E_UNSUPPORTED),  # more than 8 suspended levels
+    (dict(n_rays=512, depth_max=10), capi.IPT_E_UNSUPPORTED),  # 512 >> 9 = 1: 9 suspended levels (> 8)
     (dict(tile_rows=4, n_shards=3, shard_id=3), capi.IPT_E_INVALID),
     (dict(tile_rows=4, n_shards=3, shard_id=-1), capi.IPT_E_INVALID),
 ]
